@@ -1,0 +1,130 @@
+/*
+ * niidmix.h — C-ABI of the MI355X (gfx950) neighbour parameter-mixing library (libniidmix.so).
+ *
+ * The reference hot path is D-SGD's per-round Jacobi mixing
+ *     theta'_i = sum_{j in {i} u E(i)} W[j, i] * theta_j
+ * implemented in Python/ATen by
+ *     d_sgd.average           /root/reference/tools/simulate/algorithm/d_sgd.py:96-116
+ *     setup.model.average     /root/reference/tools/setup/model/__init__.py:15-25
+ *     d_sgd.update_models     /root/reference/tools/simulate/algorithm/d_sgd.py:29-35
+ * over the topology produced by setup.topology.load
+ *     /root/reference/tools/setup/topology/__init__.py:4-12 (edges {int: list}, weights fp32 [N,N]).
+ *
+ * The reference has no FFI of its own (it is pure Python); the binding a maintainer adds is a ctypes
+ * stub.  Every entry point below:
+ *   - takes plain device pointers and sizes (no torch types), caller-owned buffers;
+ *   - is stream-ordered on the given hipStream_t (passed as void*; NULL = default stream), never
+ *     synchronises the host, never allocates;
+ *   - returns NIIDMIX_OK or an error code; niidmix_last_error() gives a thread-local message.
+ * Slabs are row-major fp32 [rows, p] with leading dimension ld (elements).  One row = the flattened
+ * parameters of one simulated node in model.parameters() order.
+ * Jacobi semantics: every output row is computed from the pre-round input, so x and y must not
+ * overlap (checked: NIIDMIX_EALIAS).
+ */
+#ifndef NIIDMIX_H
+#define NIIDMIX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NIIDMIX_ABI_VERSION 1
+
+enum niidmix_status {
+    NIIDMIX_OK = 0,
+    NIIDMIX_EINVAL = 1,       /* bad size / pointer / mode argument */
+    NIIDMIX_EALIAS = 2,       /* input and output slabs overlap (Jacobi semantics violated) */
+    NIIDMIX_EHIP = 3,         /* a HIP runtime call failed (launch error) */
+    NIIDMIX_EUNSUPPORTED = 4  /* the plan exceeds what the kernel supports (e.g. clique too large) */
+};
+
+enum niidmix_mode {
+    /* Bit-exact with the reference loop: for each row, z = x_self*0, acc = z, then in CSR order
+     * acc = fl(acc + fl(w*x_j)) (no FMA), finally y = fl(z + acc).  This is setup.model.average's
+     * deepcopy/mul_(0)/add_(w*p) (model/__init__.py:19-24) followed by update_models'
+     * p.mul_(0.); p.add_(new) (d_sgd.py:31-34). */
+    NIIDMIX_MODE_EXACT = 0,
+    /* Same terms, fused multiply-add, any association: within the north-star's 1e-5 relative
+     * (condition-aware) tolerance, not bitwise. */
+    NIIDMIX_MODE_FAST = 1
+};
+
+/* OR-ed into `mode`: write the averaged model itself (setup.model.average's return value,
+ * model/__init__.py:25) instead of the update_models epilogue fl(x_self*0 + avg).  The two differ
+ * only in the sign of an exactly-zero result. */
+#define NIIDMIX_FLAG_AVERAGE_ONLY 2
+
+/* ABI version (NIIDMIX_ABI_VERSION). */
+int niidmix_abi_version(void);
+
+/* Thread-local description of the last error returned on this thread ("" if none). */
+const char *niidmix_last_error(void);
+
+/* Sparse mixing over a CSR of W^T rows, in the reference's accumulation order.
+ * Replaces d_sgd.average (d_sgd.py:96-116) + setup.model.average (model/__init__.py:15-25)
+ * + update_models (d_sgd.py:29-35) for all nodes of one round.
+ *   x        [>= max(col)+1, ld_x] input slab (device)
+ *   y        [n_rows, ld_y] output slab (device), must not overlap x
+ *   row_ptr  [n_rows+1] int64 (device); row r's entries are [row_ptr[r], row_ptr[r+1])
+ *   col      [nnz] int32 input-row indices (device); the FIRST entry of each row is the node itself
+ *            (the reference's models[0] = self, d_sgd.py:105)
+ *   val      [nnz] fp32 weights (device): val = W[src, rank] (d_sgd.py:106), self weight first
+ *   mode     NIIDMIX_MODE_EXACT or NIIDMIX_MODE_FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY
+ * Rows with no entries are written as +0. */
+int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                        int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,
+                        int mode, void *stream);
+
+/* Clique-factored mixing (fast mode only).  For each member m of clique c:
+ *   y_m = a_m * x_m + sum_{g < n_groups} c_{m,g} * S_{c,g} + sum_r res_val[r] * x[res_col[r]]
+ * with S_{c,g} = sum of x over the members of clique c in group g.  The host derives the plan from
+ * the loaded W (topology.json 'cliques', d_cliques/random_cliques.py:18-37 + weights.py:15-25) and
+ * verifies that it reproduces every W entry; see DESIGN.md.  All arrays are device pointers.
+ *   clique_ptr   [n_cliques+1] int32 offsets into the member arrays
+ *   member_row   [n_members] int32 row index (input row == output row)
+ *   member_group [n_members] int32 group id in [0, n_groups)
+ *   coef         [n_members * (1 + n_groups)] fp32: a_m, then c_{m,0..n_groups-1}
+ *   res_ptr      [n_members+1] int32 offsets into res_col/res_val (residual sparse terms)
+ *   res_col      [n_res] int32 input rows, res_val [n_res] fp32
+ *   max_clique   largest clique size (selects the register tile; <= 256 supported)
+ *   n_groups     1..4 */
+typedef struct niidmix_clique_plan {
+    int32_t n_cliques;
+    int32_t n_members;
+    int32_t n_groups;
+    int32_t max_clique;
+    const int32_t *clique_ptr;
+    const int32_t *member_row;
+    const int32_t *member_group;
+    const float *coef;
+    const int32_t *res_ptr;
+    const int32_t *res_col;
+    const float *res_val;
+} niidmix_clique_plan;
+
+int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                           const niidmix_clique_plan *plan, void *stream);
+
+/* Dense mixing Y = W^T X on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), for topologies dense
+ * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).
+ *   w  [n, n] fp32 row-major, w[src*n + dst] = W[src, dst] — the reference's topology['weights']
+ *      layout (topology/__init__.py:9) — device pointer
+ *   x  [n, ld_x], y [n, ld_y] */
+int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
+                          int64_t p, const float *w, void *stream);
+
+/* Column mean over rows (the uniform global average of setup.model.average(models) with
+ * weights=None, model/__init__.py:17-18, used by d_sgd.init :137-141 and the logger :112,260),
+ * with the per-row squared L2 distance to that mean (logger.model_distance, logger.py:42-48).
+ *   mean  [p] fp32 output;  dist2 [n] fp64 output (may be NULL)
+ *   mode EXACT reproduces the reference's left-to-right fl(acc + fl(w*x_k)) with w = fp32(1/n). */
+int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, float *mean,
+                          double *dist2, int mode, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NIIDMIX_H */

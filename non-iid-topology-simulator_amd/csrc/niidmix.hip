@@ -1,0 +1,533 @@
+// niidmix.hip — gfx950 (MI355X, CDNA4) kernels for D-SGD neighbour parameter mixing and the C-ABI
+// declared in include/niidmix.h.
+//
+// Reference hot path (what these kernels replace, one launch per round for ALL nodes):
+//   d_sgd.average        /root/reference/tools/simulate/algorithm/d_sgd.py:96-116
+//   setup.model.average  /root/reference/tools/setup/model/__init__.py:15-25
+//   update_models        /root/reference/tools/simulate/algorithm/d_sgd.py:29-35
+//
+// Data layout: the N simulated nodes' flattened models are one row-major fp32 slab [N, ld] in HBM
+// (row = node, flattened in model.parameters() order).  Mixing is out-of-place (x -> y ping-pong)
+// because the reference computes every average from pre-round parameters before overwriting any
+// model (Jacobi).
+//
+// This translation unit is compiled with -ffp-contract=off: every a*b+c below is two roundings
+// unless written as __builtin_fmaf.  The exact kernel relies on that for bit-exactness with the
+// reference's separate ATen mul and add_ (model/__init__.py:24: c1.add_(w*p1)).
+//
+// Kernels:
+//   k_mix_csr<EXACT,VEC>   generic CSR gather, one wave per (output row, 256-column chunk);
+//                          XCD-aware work order so the rows one chunk needs stay in that XCD's L2.
+//   k_mix_clique<RPW,G>    clique-factored: one 512-thread workgroup per (clique, 256-column chunk)
+//                          reads each member row ONCE from HBM into registers, forms the per-group
+//                          clique sums with a cross-wave LDS reduction, writes each output once.
+//                          HBM-bound: 2*4 bytes per node-parameter.
+//   k_mix_dense            Y = W^T X on v_mfma_f32_32x32x2_f32 (fp32 matrix cores), 128x128 tiles.
+//   k_mean_cols / k_row_dist2   uniform average + squared distance to it (consensus distance).
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/niidmix.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+thread_local char g_last_error[512] = "";
+
+int set_error(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(NIIDMIX_EHIP, "%s: %s", what, hipGetErrorString(e));
+    g_last_error[0] = '\0';
+    return NIIDMIX_OK;
+}
+
+constexpr int kWave = 64;
+constexpr int64_t kChunk = 256;  // fp32 columns per (row, chunk) work item: 64 lanes x float4
+constexpr int64_t kMaxGrid = 8 * 16384;  // grid-stride cap, multiple of 8 (keeps t % 8 fixed)
+
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+__device__ __forceinline__ void st4_nt(float *p, float4 v) {
+    __builtin_nontemporal_store(v.x, p + 0);
+    __builtin_nontemporal_store(v.y, p + 1);
+    __builtin_nontemporal_store(v.z, p + 2);
+    __builtin_nontemporal_store(v.w, p + 3);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Exact / fast per-element update rules.
+//   exact: acc = fl(acc + fl(w*x))      (ATen CPU add_(w*p): separate roundings, no FMA)
+//   fast : acc = fma(w, x, acc)
+template <bool EXACT>
+__device__ __forceinline__ float axpy(float w, float xv, float acc) {
+    if constexpr (EXACT) {
+        const float t = w * xv;  // rounded (fp-contract=off)
+        return acc + t;
+    } else {
+        return __builtin_fmaf(w, xv, acc);
+    }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float4 axpy4(float w, float4 xv, float4 acc) {
+    return make_float4(axpy<EXACT>(w, xv.x, acc.x), axpy<EXACT>(w, xv.y, acc.y),
+                       axpy<EXACT>(w, xv.z, acc.z), axpy<EXACT>(w, xv.w, acc.w));
+}
+
+// ----------------------------------------------------------------------------------------------
+// Generic CSR mixing.  Work item = (group of 4 output rows, chunk of 256 columns); each wave owns
+// one output row.  Work order is XCD-aware: items t and t+8 share an XCD (round-robin dispatch),
+// and consecutive items on one XCD sweep all rows of the SAME chunk, so the chunk's source rows
+// (rows x 1 KiB) are reused from that XCD's L2 by every output row that gathers them.
+template <bool EXACT, bool VEC>
+__global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, int64_t ld_x,
+                                                 float *__restrict__ y, int64_t ld_y,
+                                                 int64_t n_rows, int64_t p,
+                                                 const int64_t *__restrict__ row_ptr,
+                                                 const int32_t *__restrict__ col,
+                                                 const float *__restrict__ val,
+                                                 int64_t n_row_groups, int64_t n_items,
+                                                 int avg_only) {
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t chunk = (local / n_row_groups) * 8 + xcd;
+        const int64_t row = (local % n_row_groups) * 4 + wave;
+        const int64_t c0 = chunk * kChunk;
+        if (row >= n_rows || c0 >= p) continue;  // wave-uniform
+        const int64_t beg = row_ptr[row];
+        const int64_t end = row_ptr[row + 1];
+        if constexpr (VEC) {
+            const int64_t c = c0 + 4 * lane;
+            if (c >= p) continue;
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (beg < end) {
+                const float4 xs = ld4(x + (int64_t)col[beg] * ld_x + c);
+                // self * 0: keeps -0.0 and turns inf/NaN into NaN, as p.mul_(0) does
+                z = make_float4(xs.x * 0.f, xs.y * 0.f, xs.z * 0.f, xs.w * 0.f);
+            }
+            float4 acc = z;
+            int64_t k = beg;
+            for (; k + 8 <= end; k += 8) {  // 8 independent loads in flight, then in-order accumulate
+                float4 xv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = ld4(x + (int64_t)col[k + u] * ld_x + c);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = axpy4<EXACT>(val[k + u], xv[u], acc);
+            }
+            for (; k < end; ++k) acc = axpy4<EXACT>(val[k], ld4(x + (int64_t)col[k] * ld_x + c), acc);
+            // update_models: p.mul_(0.); p.add_(new)  ->  z + acc
+            const float4 out = avg_only ? acc : make_float4(z.x + acc.x, z.y + acc.y, z.z + acc.z, z.w + acc.w);
+            st4_nt(y + row * ld_y + c, out);
+        } else {
+            // scalar columns: lane handles c0 + lane + 64*q, q = 0..3 (coalesced per q)
+            float z[4], acc[4];
+            bool ok[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t c = c0 + lane + 64 * q;
+                ok[q] = c < p;
+                z[q] = 0.f;
+                if (ok[q] && beg < end) z[q] = x[(int64_t)col[beg] * ld_x + c] * 0.f;
+                acc[q] = z[q];
+            }
+            for (int64_t k = beg; k < end; ++k) {
+                const float w = val[k];
+                const float *src = x + (int64_t)col[k] * ld_x;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (ok[q]) acc[q] = axpy<EXACT>(w, src[c0 + lane + 64 * q], acc[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (ok[q]) y[row * ld_y + c0 + lane + 64 * q] = avg_only ? acc[q] : z[q] + acc[q];
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Clique-factored mixing (fast mode).  Work item = (clique, 256-column chunk); 8 waves; wave w holds
+// members w, w+8, w+16, ... (RPW rows per wave, float4 per lane per row) in registers.
+//   1. every member row is loaded once (all loads issued before the first use),
+//   2. per-wave partial group sums -> LDS -> every wave forms the full clique group sums S_g,
+//   3. y_m = a_m x_m + sum_g c_{m,g} S_g + residual terms (gateway edges), stored once.
+// Work order is XCD-aware (cliques of one chunk are consecutive on one XCD) so the residual rows a
+// gateway gathers from another clique are usually still in that XCD's L2.
+constexpr int kCliqueWaves = 8;
+
+template <int RPW, int G>
+__global__ __launch_bounds__(512) void k_mix_clique(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
+    const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
+    const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
+    __shared__ float4 red[G][kCliqueWaves][kWave];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t chunk = (local / n_cliques) * 8 + xcd;
+        const int32_t cq = (int32_t)(local % n_cliques);
+        const int64_t c = chunk * kChunk + 4 * lane;
+        const bool valid_chunk = chunk * kChunk < p;  // block-uniform
+        const bool act = c < p;
+        const int32_t m0 = clique_ptr[cq];
+        const int32_t M = valid_chunk ? clique_ptr[cq + 1] - m0 : 0;
+
+        float4 v[RPW];
+        float4 s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int k = wave + kCliqueWaves * r;
+            v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k < M && act) v[r] = ld4(x + (int64_t)member_row[m0 + k] * ld_x + c);
+        }
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int k = wave + kCliqueWaves * r;
+            if (k < M) {
+                const int g = member_group[m0 + k];
+#pragma unroll
+                for (int gg = 0; gg < G; ++gg)
+                    if (g == gg) {
+                        s[gg].x += v[r].x; s[gg].y += v[r].y; s[gg].z += v[r].z; s[gg].w += v[r].w;
+                    }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float4 a = red[g][0][lane];
+#pragma unroll
+            for (int w = 1; w < kCliqueWaves; ++w) {
+                const float4 b = red[g][w][lane];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            s[g] = a;
+        }
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int k = wave + kCliqueWaves * r;
+            if (k < M) {
+                const int32_t m = m0 + k;
+                const float *cf = coef + (int64_t)m * (1 + G);
+                const float a = cf[0];
+                float4 o = make_float4(a * v[r].x, a * v[r].y, a * v[r].z, a * v[r].w);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const float cg = cf[1 + g];
+                    o.x = __builtin_fmaf(cg, s[g].x, o.x);
+                    o.y = __builtin_fmaf(cg, s[g].y, o.y);
+                    o.z = __builtin_fmaf(cg, s[g].z, o.z);
+                    o.w = __builtin_fmaf(cg, s[g].w, o.w);
+                }
+                const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
+                if (act) {
+                    for (int32_t q = rb; q < re; ++q) {
+                        const float4 xr = ld4(x + (int64_t)res_col[q] * ld_x + c);
+                        o = axpy4<false>(res_val[q], xr, o);
+                    }
+                    st4_nt(y + (int64_t)member_row[m] * ld_y + c, o);
+                }
+            }
+        }
+        __syncthreads();  // red[] is reused by the next work item
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Dense Y = W^T X on fp32 MFMA.  Block tile 128 (output rows i) x 128 (columns j), K step 16,
+// 4 waves in 2x2, each wave 64x64 = 2x2 tiles of v_mfma_f32_32x32x2_f32.
+//   A[i][k] = W[k0+k][i0+i]  (LDS As[k][i]);  B[k][j] = X[k0+k][j0+j]  (LDS Bs[k][j])
+//   operand maps (32x32x2 f32): lane l holds A[l&31][l>>5], B[l>>5][l&31];
+//   C/D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15.
+constexpr int kDBM = 128, kDBN = 128, kDBK = 16, kDPad = 4;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
+                                                   float *__restrict__ y, int64_t ld_y, int64_t n,
+                                                   int64_t p, const float *__restrict__ w,
+                                                   int64_t n_it, int64_t n_items) {
+    __shared__ float As[kDBK][kDBM + kDPad];
+    __shared__ float Bs[kDBK][kDBN + kDPad];
+    const int tid = threadIdx.x;
+    const int wave = wave_id();
+    const int lane = tid & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t jt = (local / n_it) * 8 + xcd;
+        const int64_t it = local % n_it;
+        const int64_t i0 = it * kDBM, j0 = jt * kDBN;
+        if (j0 >= p) continue;  // block-uniform
+        floatx16 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+        // loader mapping: 16 rows x 128 cols = 2048 floats, 8 per thread as 2 x float4
+        const int lk = tid >> 4;          // 0..15
+        const int lc = (tid & 15) * 8;    // 0..120
+        for (int64_t k0 = 0; k0 < n; k0 += kDBK) {
+            float ra[8], rb[8];
+            const int64_t kr = k0 + lk;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + lc + u;
+                ra[u] = (kr < n && i < n) ? w[kr * n + i] : 0.f;
+            }
+            if (VEC) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int64_t j = j0 + lc + 4 * h;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (kr < n && j < p) v = ld4(x + kr * ld_x + j);
+                    rb[4 * h + 0] = v.x; rb[4 * h + 1] = v.y; rb[4 * h + 2] = v.z; rb[4 * h + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t j = j0 + lc + u;
+                    rb[u] = (kr < n && j < p) ? x[kr * ld_x + j] : 0.f;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                As[lk][lc + u] = ra[u];
+                Bs[lk][lc + u] = rb[u];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int kk = 0; kk < kDBK; kk += 2) {
+                const int kq = kk + (lane >> 5);
+                float a0 = As[kq][wm * 64 + (lane & 31)];
+                float a1 = As[kq][wm * 64 + 32 + (lane & 31)];
+                float b0 = Bs[kq][wn * 64 + (lane & 31)];
+                float b1 = Bs[kq][wn * 64 + 32 + (lane & 31)];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int64_t j = j0 + wn * 64 + b * 32 + (lane & 31);
+                    if (i < n && j < p) y[i * ld_y + j] = acc[a][b][r];
+                }
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Uniform average over rows (model/__init__.py:17-24 with weights=None): one lane per column,
+// left-to-right over rows.  EXACT: mean = fl(...fl(fl(x0*0) + fl(w x0)) + ...), w = fp32(1/n).
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_mean_cols(const float *__restrict__ x, int64_t ld_x,
+                                                   int64_t n, int64_t p, float w,
+                                                   float *__restrict__ mean) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < p;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        float acc = n > 0 ? x[c] * 0.f : 0.f;
+        int64_t k = 0;
+        for (; k + 8 <= n; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = x[(k + u) * ld_x + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = axpy<EXACT>(w, v[u], acc);
+        }
+        for (; k < n; ++k) acc = axpy<EXACT>(w, x[k * ld_x + c], acc);
+        mean[c] = acc;
+    }
+}
+
+// Squared L2 distance of every row to the mean (logger.model_distance, logger.py:42-48), fp64
+// accumulation, one workgroup per row, deterministic order.
+__global__ __launch_bounds__(256) void k_row_dist2(const float *__restrict__ x, int64_t ld_x,
+                                                   int64_t p, const float *__restrict__ mean,
+                                                   double *__restrict__ dist2) {
+    __shared__ double part[256];
+    const int64_t row = blockIdx.x;
+    double acc = 0.0;
+    for (int64_t c = threadIdx.x; c < p; c += blockDim.x) {
+        const double d = (double)x[row * ld_x + c] - (double)mean[c];
+        acc += d * d;
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dist2[row] = part[0];
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int64_t grid_for(int64_t items) { return items < kMaxGrid ? ((items + 7) / 8) * 8 : kMaxGrid; }
+
+bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) {
+    return a < b + b_elems && b < a + a_elems;
+}
+
+template <int RPW, int G>
+void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                   const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
+    const int64_t grid = grid_for(n_items);
+    hipLaunchKernelGGL((k_mix_clique<RPW, G>), dim3((unsigned)grid), dim3(512), 0, s, x, ld_x, y,
+                       ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group,
+                       pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_items);
+}
+
+template <int RPW>
+int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
+    switch (pl->n_groups) {
+        case 1: launch_clique<RPW, 1>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 2: launch_clique<RPW, 2>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 3: launch_clique<RPW, 3>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 4: launch_clique<RPW, 4>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
+    }
+    return check_launch("k_mix_clique");
+}
+
+}  // namespace
+
+extern "C" {
+
+int niidmix_abi_version(void) { return NIIDMIX_ABI_VERSION; }
+
+const char *niidmix_last_error(void) { return g_last_error; }
+
+int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                        int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,
+                        int mode, void *stream) {
+    if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (n_rows == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !row_ptr || !col || !val) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (x == y || (x > y && x < y + (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool vec = (p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y);
+    const int64_t n_chunks = (p + kChunk - 1) / kChunk;
+    const int64_t n_row_groups = (n_rows + 3) / 4;
+    const int64_t n_items = n_row_groups * ((n_chunks + 7) / 8) * 8;
+    const dim3 grid((unsigned)grid_for(n_items)), block(256);
+    if (mode == NIIDMIX_MODE_EXACT) {
+        if (vec) hipLaunchKernelGGL((k_mix_csr<true, true>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+        else     hipLaunchKernelGGL((k_mix_csr<true, false>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_mix_csr<false, true>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+        else     hipLaunchKernelGGL((k_mix_csr<false, false>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+    }
+    return check_launch("k_mix_csr");
+}
+
+int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                           const niidmix_clique_plan *plan, void *stream) {
+    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
+    if (p < 0 || plan->n_cliques < 0 || plan->n_members < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (plan->n_cliques == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !plan->clique_ptr || !plan->member_row || !plan->member_group || !plan->coef ||
+        !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0))
+        return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))
+        return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n_chunks = (p + kChunk - 1) / kChunk;
+    const int64_t n_items = (int64_t)plan->n_cliques * ((n_chunks + 7) / 8) * 8;
+    const int mc = plan->max_clique;
+    if (mc <= 16) return launch_clique_g<2>(x, ld_x, y, ld_y, p, plan, n_items, s);
+    if (mc <= 32) return launch_clique_g<4>(x, ld_x, y, ld_y, p, plan, n_items, s);
+    if (mc <= 64) return launch_clique_g<8>(x, ld_x, y, ld_y, p, plan, n_items, s);
+    if (mc <= 128) return launch_clique_g<16>(x, ld_x, y, ld_y, p, plan, n_items, s);
+    if (mc <= 256) return launch_clique_g<32>(x, ld_x, y, ld_y, p, plan, n_items, s);
+    return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
+}
+
+int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
+                          int64_t p, const float *w, void *stream) {
+    if (n < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !w) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (overlaps(x, (n - 1) * ld_x + p, y, (n - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool vec = (p % 4 == 0) && (ld_x % 4 == 0) && aligned16(x);
+    const int64_t n_it = (n + kDBM - 1) / kDBM;
+    const int64_t n_jt = (p + kDBN - 1) / kDBN;
+    const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
+    const dim3 grid((unsigned)grid_for(n_items)), block(256);
+    if (vec) hipLaunchKernelGGL((k_mix_dense<true>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items);
+    else     hipLaunchKernelGGL((k_mix_dense<false>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items);
+    return check_launch("k_mix_dense");
+}
+
+int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, float *mean,
+                          double *dist2, int mode, void *stream) {
+    if (n < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (n == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !mean) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (overlaps(x, (n - 1) * ld_x + p, mean, p)) return set_error(NIIDMIX_EALIAS, "mean overlaps x");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const float w = (float)(1.0 / (double)n);
+    const int64_t blocks = (p + 255) / 256 < 16384 ? (p + 255) / 256 : 16384;
+    if (mode == NIIDMIX_MODE_EXACT)
+        hipLaunchKernelGGL((k_mean_cols<true>), dim3((unsigned)blocks), dim3(256), 0, s, x, ld_x, n, p, w, mean);
+    else
+        hipLaunchKernelGGL((k_mean_cols<false>), dim3((unsigned)blocks), dim3(256), 0, s, x, ld_x, n, p, w, mean);
+    int rc = check_launch("k_mean_cols");
+    if (rc != NIIDMIX_OK || !dist2) return rc;
+    hipLaunchKernelGGL(k_row_dist2, dim3((unsigned)n), dim3(256), 0, s, x, ld_x, p, mean, dist2);
+    return check_launch("k_row_dist2");
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+"""ctypes binding of libniidmix.so (the C-ABI in include/niidmix.h).
+
+This is the same stub a maintainer would add to the reference.  There is NO CPU
+fallback: if the HIP library is missing the import fails loudly.
+
+torch is imported first on purpose: torch ships its own libamdhip64.so (SONAME libamdhip64.so.7);
+once it is loaded, the dynamic loader binds libniidmix.so to that same HIP runtime, so device
+pointers and hipStream_t handles coming from torch are valid in our calls.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before libniidmix.so, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NIIDMIX_LIB", os.path.join(_HERE, "libniidmix.so"))
+
+OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
+MODE_EXACT, MODE_FAST = 0, 1
+ABI_VERSION = 1
+
+_i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+
+
+class CliquePlanC(ctypes.Structure):
+    """Mirror of struct niidmix_clique_plan (include/niidmix.h)."""
+    _fields_ = [("n_cliques", _i32), ("n_members", _i32), ("n_groups", _i32), ("max_clique", _i32),
+                ("clique_ptr", _vp), ("member_row", _vp), ("member_group", _vp), ("coef", _vp),
+                ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp)]
+
+
+# every symbol include/niidmix.h declares, with its ctypes signature
+SIGNATURES = {
+    "niidmix_abi_version": (ctypes.c_int, []),
+    "niidmix_last_error": (ctypes.c_char_p, []),
+    "niidmix_mix_csr_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
+                                           ctypes.c_int, _vp]),
+    "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+                                              ctypes.POINTER(CliquePlanC), _vp]),
+    "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
+}
+
+
+class NiidmixError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libniidmix.so not found at {LIB_PATH}: build it with `python -m niidmix.build` "
+            "(or __graft_entry__.build()); there is no CPU fallback for the mixing kernels")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.niidmix_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"libniidmix.so ABI {v} != expected {ABI_VERSION}; rebuild it")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != OK:
+        msg = lib.niidmix_last_error().decode(errors="replace")
+        raise NiidmixError(f"{what}: niidmix error {rc}: {msg}")

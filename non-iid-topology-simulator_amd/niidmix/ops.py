@@ -1,0 +1,215 @@
+"""PyTorch-ROCm custom ops over libniidmix.so, and the Mixer that picks a kernel per topology.
+
+Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
+  mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
+  mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, out,
+             max_clique)                            k_mix_clique (fast, HBM-bound)
+  mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
+  mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
+All ops launch on torch's current HIP stream of the input's device, never synchronise, and raise
+RuntimeError (TORCH_CHECK-style) on bad arguments.  They accept HIP tensors only: there is no CPU
+implementation and no fallback.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .factor import build_clique_plan
+from .topology import MixCSR, to_csr
+
+EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
+AVERAGE_ONLY = 2
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _req(cond, msg):
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _slab(name, t, rows=None, cols=None):
+    _req(isinstance(t, torch.Tensor), f"{name}: expected a tensor")
+    _req(t.is_cuda, f"{name}: expected a HIP (cuda) tensor, got {t.device} (no CPU fallback)")
+    _req(t.dtype == torch.float32, f"{name}: expected float32, got {t.dtype}")
+    _req(t.dim() == 2, f"{name}: expected a 2-D [rows, p] slab")
+    _req(t.stride(1) == 1 or t.shape[1] <= 1, f"{name}: rows must be contiguous (stride(1) == 1)")
+    if rows is not None:
+        _req(t.shape[0] == rows, f"{name}: expected {rows} rows, got {t.shape[0]}")
+    if cols is not None:
+        _req(t.shape[1] == cols, f"{name}: expected {cols} columns, got {t.shape[1]}")
+
+
+def _vec(name, t, dtype, device, n=None):
+    _req(t.device == device, f"{name}: must be on {device}")
+    _req(t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}")
+    _req(t.dim() == 1 and t.is_contiguous(), f"{name}: expected a contiguous 1-D tensor")
+    if n is not None:
+        _req(t.numel() == n, f"{name}: expected {n} elements, got {t.numel()}")
+
+
+def _no_overlap(a, b):
+    if a.numel() == 0 or b.numel() == 0:
+        return
+    sa, sb = a.untyped_storage(), b.untyped_storage()
+    if sa.data_ptr() != sb.data_ptr():
+        return
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    a1 = a0 + ((a.shape[0] - 1) * a.stride(0) + a.shape[1]) * 4
+    b1 = b0 + ((b.shape[0] - 1) * b.stride(0) + b.shape[1]) * 4
+    _req(a1 <= b0 or b1 <= a0, "x and out overlap: mixing is out-of-place (Jacobi, d_sgd.py:99-116)")
+
+
+def _ld(t):
+    return t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
+
+
+@torch.library.custom_op("niidmix::mix_csr", mutates_args=("out",))
+def mix_csr(x: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
+            out: torch.Tensor, mode: int) -> None:
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    _req(out.device == x.device, "x and out must be on the same device")
+    n = out.shape[0]
+    _vec("row_ptr", row_ptr, torch.int64, x.device, n + 1)
+    _vec("col", col, torch.int32, x.device)
+    _vec("val", val, torch.float32, x.device, col.numel())
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_csr_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n, x.shape[1],
+                                      row_ptr.data_ptr(), col.data_ptr(), val.data_ptr(), int(mode),
+                                      _stream(x))
+    _lib.check(rc, "niidmix::mix_csr")
+
+
+@torch.library.custom_op("niidmix::mix_clique", mutates_args=("out",))
+def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
+               member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
+               res_col: torch.Tensor, res_val: torch.Tensor, out: torch.Tensor,
+               max_clique: int) -> None:
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    dev = x.device
+    _vec("clique_ptr", clique_ptr, torch.int32, dev)
+    m = member_row.numel()
+    _vec("member_row", member_row, torch.int32, dev)
+    _vec("member_group", member_group, torch.int32, dev, m)
+    _req(coef.device == dev and coef.dtype == torch.float32 and coef.dim() == 2 and
+         coef.shape[0] == m and coef.is_contiguous(), "coef: expected contiguous fp32 [M, 1+G]")
+    g = coef.shape[1] - 1
+    _req(1 <= g <= 4, "coef: 1..4 groups supported")
+    _vec("res_ptr", res_ptr, torch.int32, dev, m + 1)
+    _vec("res_col", res_col, torch.int32, dev)
+    _vec("res_val", res_val, torch.float32, dev, res_col.numel())
+    _no_overlap(x, out)
+    plan = _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), clique_ptr.data_ptr(),
+                            member_row.data_ptr(), member_group.data_ptr(), coef.data_ptr(),
+                            res_ptr.data_ptr(), res_col.data_ptr() if res_col.numel() else
+                            res_ptr.data_ptr(), res_val.data_ptr() if res_val.numel() else
+                            coef.data_ptr())
+    rc = _lib.lib.niidmix_mix_clique_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
+                                         ctypes.byref(plan), _stream(x))
+    _lib.check(rc, "niidmix::mix_clique")
+
+
+@torch.library.custom_op("niidmix::mix_dense", mutates_args=("out",))
+def mix_dense(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
+    _slab("x", x)
+    n = x.shape[0]
+    _slab("out", out, rows=n, cols=x.shape[1])
+    _req(w.device == x.device and w.dtype == torch.float32 and w.shape == (n, n) and
+         w.is_contiguous(), "w: expected contiguous fp32 [N, N] (W[src, dst])")
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_dense_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n,
+                                        x.shape[1], w.data_ptr(), _stream(x))
+    _lib.check(rc, "niidmix::mix_dense")
+
+
+@torch.library.custom_op("niidmix::mean_rows", mutates_args=("mean", "dist2"))
+def mean_rows(x: torch.Tensor, mean: torch.Tensor, dist2: torch.Tensor, mode: int) -> None:
+    _slab("x", x)
+    _req(mean.device == x.device and mean.dtype == torch.float32 and mean.numel() == x.shape[1]
+         and mean.is_contiguous(), "mean: expected contiguous fp32 [p]")
+    want_d = dist2.numel() > 0
+    if want_d:
+        _req(dist2.device == x.device and dist2.dtype == torch.float64 and
+             dist2.numel() == x.shape[0], "dist2: expected fp64 [n] (or empty)")
+    rc = _lib.lib.niidmix_mean_rows_f32(x.data_ptr(), _ld(x), x.shape[0], x.shape[1],
+                                        mean.data_ptr(), dist2.data_ptr() if want_d else None,
+                                        int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mean_rows")
+
+
+# ------------------------------------------------------------------------------------------------
+class Mixer:
+    """One topology's mixing operator on one device: Θ' = Wᵀ Θ for a [N, P] fp32 slab.
+
+    kernel='auto' picks (fast mode):  clique-factored if the topology factors over its cliques
+    (factor.py), else dense MFMA if W is dense (nnz >= dense_threshold * N^2), else CSR gather.
+    mode='exact' always uses the bit-exact CSR kernel (the reference's operand order).
+    """
+
+    def __init__(self, topology=None, *, csr=None, cliques=None, device="cuda",
+                 dense_threshold=0.25, factor=True):
+        if csr is None:
+            csr = to_csr(topology)
+        if cliques is None and topology is not None:
+            cliques = topology.get("cliques")
+        self.csr = csr
+        self.n = csr.n
+        self.device = torch.device(device)
+        dev = self.device
+        self.row_ptr = torch.from_numpy(csr.row_ptr).to(dev)
+        self.col = torch.from_numpy(csr.col).to(dev)
+        self.val = torch.from_numpy(csr.val).to(dev)
+        self.plan, self.plan_reason = (None, "factorisation disabled")
+        if factor:
+            self.plan, self.plan_reason = build_clique_plan(csr, cliques)
+        if self.plan is not None:
+            p = self.plan
+            self.p_clique_ptr = torch.from_numpy(p.clique_ptr).to(dev)
+            self.p_member_row = torch.from_numpy(p.member_row).to(dev)
+            self.p_member_group = torch.from_numpy(p.member_group).to(dev)
+            self.p_coef = torch.from_numpy(np.ascontiguousarray(p.coef)).to(dev)
+            self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
+            self.p_res_col = torch.from_numpy(p.res_col).to(dev)
+            self.p_res_val = torch.from_numpy(p.res_val).to(dev)
+        self.dense = csr.nnz >= dense_threshold * self.n * self.n and self.n >= 64
+        self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
+
+    def kernel_for(self, mode="fast", x=None):
+        if mode == "exact":
+            return "csr-exact"
+        if self.plan is not None and (x is None or (x.shape[1] % 4 == 0 and _ld(x) % 4 == 0)):
+            return "clique"
+        if self.dense:
+            return "dense"
+        return "csr-fast"
+
+    def __call__(self, x, out=None, mode="fast", kernel=None):
+        if out is None:
+            out = torch.empty((self.n, x.shape[1]), dtype=torch.float32, device=x.device)
+        k = kernel or self.kernel_for(mode, x)
+        if k == "csr-exact":
+            mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT)
+        elif k == "csr-fast":
+            mix_csr(x, self.row_ptr, self.col, self.val, out, FAST)
+        elif k == "clique":
+            _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
+            mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
+                       self.p_res_ptr, self.p_res_col, self.p_res_val, out, self.plan.max_clique)
+        elif k == "dense":
+            w = self.w_dense if self.w_dense is not None else \
+                torch.from_numpy(self.csr.dense()).to(x.device)
+            mix_dense(x, w, out)
+        else:
+            raise ValueError(f"unknown kernel {k!r}")
+        return out
+
+
+def csr_from_numpy(row_ptr, col, val):
+    return MixCSR(np.asarray(row_ptr, np.int64), np.asarray(col, np.int32),
+                  np.asarray(val, np.float32)).validate()

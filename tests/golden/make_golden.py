@@ -1,0 +1,240 @@
+#!/usr/bin/env python
+"""Generate the golden mixing fixtures by running the REFERENCE simulator's own code.
+
+Run in the development container only (it needs /root/reference; the GPU box never runs it):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it does, per case:
+  1. builds a topology with the reference generator (tools/setup/topology/*.py,
+     tools/setup/topology/d_cliques/*.py) and its Metropolis-Hastings weights
+     (tools/setup/topology/weights.py:3-32),
+  2. writes topology.json exactly like the generators do (json.dump of
+     {'edges', 'weights', 'cliques'?}) and reads it back with the reference
+     loader `setup.topology.load` (tools/setup/topology/__init__.py:4-12),
+  3. builds one node dict per rank whose 'model' holds seeded fp32 parameters,
+  4. calls the reference hot path `simulate.algorithm.d_sgd.average`
+     (tools/simulate/algorithm/d_sgd.py:96-116) and reads the parameters back.
+
+Saved per case (tests/golden/<case>.npz):
+  x, y           fp32 [N, P] slabs before / after one round (flattening = model.parameters() order)
+  row_ptr, col, val   CSR of W^T in the reference's accumulation order: row i = [i] + edges[i],
+                      val = W[i,i], W[src,i] ...   (d_sgd.py:105-110)
+  cliques_flat, cliques_ptr   (d-cliques cases only)
+  shapes_json    parameter shapes of the model (multi-tensor case)
+Small cases additionally keep the raw topology.json (tests/golden/<case>.topology.json) so the
+build's own reader can be checked against the reference loader's output.
+
+The torchvision import in the reference's import chain (d_sgd -> setup.model -> linear ->
+setup.dataset -> torchvision) is satisfied with an empty stub: torchvision is only used for
+datasets, never by the mixing code.  Nothing from the reference is copied into this repo:
+only inputs and outputs (data) are stored.
+"""
+import io
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("NIID_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference():
+    for name in ["torchvision", "torchvision.datasets", "torchvision.transforms", "torchvision.utils"]:
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["torchvision"].datasets = sys.modules["torchvision.datasets"]
+    sys.modules["torchvision"].transforms = sys.modules["torchvision.transforms"]
+    sys.path.insert(0, os.path.join(REF, "tools"))
+    sys.path.insert(0, os.path.join(REF, "tools", "setup", "topology", "d_cliques"))
+    import importlib
+    mods = types.SimpleNamespace()
+    mods.d_sgd = importlib.import_module("simulate.algorithm.d_sgd")
+    mods.model = importlib.import_module("setup.model")
+    mods.linear = importlib.import_module("setup.model.linear")
+    mods.topo = importlib.import_module("setup.topology")
+    mods.weights = importlib.import_module("setup.topology.weights")
+    mods.metrics = importlib.import_module("setup.topology.metrics")
+    mods.ring = importlib.import_module("setup.topology.ring")
+    mods.fc = importlib.import_module("setup.topology.fully-connected")
+    mods.expander = importlib.import_module("setup.topology.expander")
+    mods.grid = importlib.import_module("setup.topology.grid")
+    mods.random_graph = importlib.import_module("setup.topology.random_graph")
+    mods.random_cliques = importlib.import_module("random_cliques")
+    mods.interclique = importlib.import_module("interclique")
+    mods.dc_utils = importlib.import_module("utils")
+    return mods
+
+
+R = _import_reference()
+MH = {"weights": "metropolis-hasting"}
+
+
+class FlatModel(torch.nn.Module):
+    """A node model whose parameters have the given shapes (registration order = flattening order)."""
+
+    def __init__(self, shapes):
+        super().__init__()
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(s)) for s in shapes])
+
+
+def _nodes(n):
+    return [{"rank": r, "classes": [0.1] * 10} for r in range(n)]
+
+
+def _roundtrip(edges, weights, cliques=None):
+    """topology.json exactly as the generators write it, read back by setup.topology.load."""
+    topo = {"edges": {rank: list(edges[rank]) for rank in edges}, "weights": weights}
+    if cliques is not None:
+        topo["cliques"] = cliques
+    text = json.dumps(topo)
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "topology.json"), "w") as f:
+            f.write(text)
+        loaded = R.topo.load(d)
+    return text, loaded
+
+
+def _csr(loaded, n):
+    W = loaded["weights"]
+    edges = loaded["edges"]
+    row_ptr = [0]
+    col, val = [], []
+    for rank in range(n):
+        srcs = [rank] + list(edges[rank])
+        col += srcs
+        val += [W[rank, rank].item()] + [W[s, rank].item() for s in edges[rank]]
+        row_ptr.append(len(col))
+    return (np.asarray(row_ptr, np.int64), np.asarray(col, np.int32), np.asarray(val, np.float32))
+
+
+def _run_average(loaded, x, shapes):
+    n = x.shape[0]
+    nodes = []
+    for rank in range(n):
+        m = FlatModel(shapes) if shapes is not None else None
+        flat = torch.from_numpy(x[rank].copy())
+        with torch.no_grad():
+            off = 0
+            for p in m.parameters():
+                k = p.numel()
+                p.copy_(flat[off:off + k].view_as(p))
+                off += k
+        nodes.append({"rank": rank, "model": m})
+    R.d_sgd.average(nodes, loaded, {})
+    out = np.stack([torch.cat([p.detach().reshape(-1) for p in nd["model"].parameters()]).numpy()
+                    for nd in nodes])
+    return out
+
+
+def save_case(name, edges, n, p, seed=0, cliques=None, shapes=None, x=None, keep_json=False,
+              weights=None):
+    if weights is None:
+        weights = R.weights.compute_weights(_nodes(n), edges, MH)
+    text, loaded = _roundtrip(edges, weights, cliques)
+    if shapes is None:
+        shapes = [(p,)]
+    assert sum(int(np.prod(s)) for s in shapes) == p
+    if x is None:
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(n, p, generator=g, dtype=torch.float32).numpy()
+    y = _run_average(loaded, x, shapes)
+    row_ptr, col, val = _csr(loaded, n)
+    extra = {}
+    if cliques is not None:
+        extra["cliques_flat"] = np.asarray([r for c in cliques for r in c], np.int32)
+        extra["cliques_ptr"] = np.cumsum([0] + [len(c) for c in cliques]).astype(np.int64)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), x=x, y=y, row_ptr=row_ptr, col=col,
+                        val=val, shapes_json=np.asarray(json.dumps([list(s) for s in shapes])),
+                        **extra)
+    if keep_json:
+        with open(os.path.join(OUT, name + ".topology.json"), "w") as f:
+            f.write(text)
+    print(f"{name}: N={n} P={p} nnz={len(col)}")
+
+
+def dcliques(n, size, interclique, seed=1337, remove=0):
+    params = {"topology": {"max-clique-size": size, "remove-clique-edges": remove,
+                           "interclique-topology": interclique},
+              "meta": {"seed": seed}, "dataset": {"nb-classes": 10}}
+    cl, intra = R.random_cliques.cliques(_nodes(n), params)
+    edges = R.interclique.get(interclique)(cl, intra, params)
+    if remove > 0:
+        edges, cl = R.dc_utils.remove_clique_edges(edges, cl, params)
+    return {rank: list(edges[rank]) for rank in edges}, [list(c) for c in cl]
+
+
+def main():
+    # 1) ring N=100, P=257 (odd tail), random metric, MH weights 1/3
+    edges = R.ring.create(_nodes(100), R.metrics.random({"seed": 1337}))
+    save_case("ring100_p257", edges, 100, 257, keep_json=True)
+
+    # 2) d-cliques N=1000: 10 cliques of 100, fully-connected interclique (reference default),
+    #    MH.  This is also the topology of the headline benchmark (BASELINE.json configs[2]).
+    e, cl = dcliques(1000, 100, "fully-connected")
+    save_case("dcliques1000_fc_p64", e, 1000, 64, cliques=cl)
+    e, cl = dcliques(1000, 100, "smallworld")
+    save_case("dcliques1000_smallworld_p16", e, 1000, 16, cliques=cl)
+    e, cl = dcliques(1000, 100, "ring")
+    save_case("dcliques1000_ring_p16", e, 1000, 16, cliques=cl)
+    # reference default clique size (30), 10 cliques, FC interclique
+    e, cl = dcliques(300, 30, "fully-connected")
+    save_case("dcliques300_fc_p37", e, 300, 37, cliques=cl, keep_json=True)
+    # clique edges removed (breaks the pure clique structure; exercises residual terms)
+    e, cl = dcliques(200, 20, "fractal", remove=5)
+    save_case("dcliques200_fractal_rm5_p40", e, 200, 40, cliques=cl, keep_json=True)
+
+    # 3) fully-connected N=64, P=33
+    edges = R.fc.create(_nodes(64))
+    save_case("fc64_p33", edges, 64, 33, keep_json=True)
+
+    # other sparse generators
+    save_case("expander64_p48", R.expander.create(_nodes(64), {}), 64, 48, keep_json=True)
+    save_case("grid49_p20", R.grid.create(_nodes(49), R.metrics.random({"seed": 1337})), 49, 20,
+              keep_json=True)
+    rg = R.random_graph.create(_nodes(50), {"topology": {"topology-seed": 1, "nb-neighbours": 5}})
+    save_case("randomgraph50_p24", rg, 50, 24, keep_json=True)
+
+    # 4) N=1 (W=[[1]], no edges) with signed zeros and non-finite values
+    x1 = np.array([[0.0, -0.0, 1.5, -2.25, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3.0e38, -3.0e38]],
+                  np.float32)
+    save_case("n1_special", {0: []}, 1, x1.shape[1], x=x1, keep_json=True)
+    #    N=2 ring (tools/tests/basic.sh shape: W = 1/2) with the linear MNIST model (7850 = [10,784]+[10])
+    edges = R.ring.create(_nodes(2), R.metrics.random({"seed": 1337}))
+    save_case("n2_ring_linear7850", edges, 2, 7850, shapes=[(10, 784), (10,)], keep_json=True)
+
+    # 5) non-finite / signed zero propagation through neighbours
+    edges = R.ring.create(_nodes(8), R.metrics.random({"seed": 1337}))
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 16, generator=g).numpy()
+    x[0, 0] = np.inf; x[1, 1] = -np.inf; x[2, 2] = np.nan; x[3, 3] = -0.0; x[3, 4] = 0.0
+    x[4, 5] = -0.0; x[5, 5] = -0.0; x[6, 5] = -0.0; x[7, 5] = -0.0; x[0, 5] = -0.0
+    x[1, 5] = -0.0; x[2, 5] = -0.0; x[3, 5] = -0.0
+    x[:, 6] = -0.0
+    x[5, 7] = np.inf; x[6, 7] = -np.inf
+    x[4, 8] = 1e-45; x[4, 9] = 3.4e38; x[5, 9] = 3.4e38
+    save_case("nonfinite_ring8_p16", edges, 8, 16, x=x, keep_json=True)
+
+    # 6) uniform global average setup.model.average(models) (weights=None -> python-float 1/K),
+    #    the primitive under d_sgd.init / logger consensus distance (model/__init__.py:15-25)
+    K, P = 7, 100
+    g = torch.Generator().manual_seed(3)
+    xu = torch.randn(K, P, generator=g).numpy()
+    models = []
+    for k in range(K):
+        m = FlatModel([(P,)])
+        with torch.no_grad():
+            m.ps[0].copy_(torch.from_numpy(xu[k]))
+        models.append(m)
+    c = R.model.average(models)
+    yu = c.ps[0].detach().numpy()[None, :]
+    np.savez_compressed(os.path.join(OUT, "uniform_avg_k7_p100.npz"), x=xu, y=yu)
+    print("uniform_avg_k7_p100")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol include/niidmix.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+from conftest import REPO
+
+
+def _declared_symbols():
+    text = open(os.path.join(REPO, "include", "niidmix.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(niidmix_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_expected_api():
+    syms = _declared_symbols()
+    for s in ["niidmix_abi_version", "niidmix_last_error", "niidmix_mix_csr_f32",
+              "niidmix_mix_clique_f32", "niidmix_mix_dense_f32", "niidmix_mean_rows_f32"]:
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from niidmix import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in _declared_symbols():
+        assert hasattr(lib, s), s
+    assert set(_lib.SIGNATURES) == set(_declared_symbols())
+    assert _lib.lib.niidmix_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_is_gfx950_code_object():
+    from niidmix import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_argument_errors_without_gpu():
+    """Validation happens before any HIP call, so errors are reported on a CPU-only host too."""
+    from niidmix import _lib
+    L = _lib.lib
+    rc = L.niidmix_mix_csr_f32(None, 4, None, 4, 1, 4, None, None, None, 0, None)
+    assert rc == _lib.EINVAL and b"null" in L.niidmix_last_error()
+    rc = L.niidmix_mix_csr_f32(16, 4, 16, 4, 1, 4, 8, 8, 8, 0, None)
+    assert rc == _lib.EALIAS
+    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 7, None)
+    assert rc == _lib.EINVAL
+    rc = L.niidmix_mix_csr_f32(16, 2, 1024, 4, 1, 4, 8, 8, 8, 0, None)
+    assert rc == _lib.EINVAL        # ld < p
+    assert L.niidmix_mix_csr_f32(16, 4, 1024, 4, 0, 4, 8, 8, 8, 0, None) == _lib.OK  # empty
+    plan = _lib.CliquePlanC(1, 4, 5, 4, 8, 8, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
+    assert rc == _lib.EUNSUPPORTED   # n_groups 5
+    plan = _lib.CliquePlanC(1, 300, 2, 300, 8, 8, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
+    assert rc == _lib.EUNSUPPORTED   # clique > 256
