@@ -89,12 +89,15 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *   res_ptr      [n_members+1] int32 offsets into res_col/res_val (residual sparse terms)
  *   res_col      [n_res] int32 input rows, res_val [n_res] fp32
  *   max_clique   largest clique size (selects the register tile; <= 256 supported)
+ *   max_clique_res  largest number of residual terms of one clique (res_ptr[end]-res_ptr[begin]
+ *                over its members); <= 64 supported (<= 16 when max_clique > 128)
  *   n_groups     1..4 */
 typedef struct niidmix_clique_plan {
     int32_t n_cliques;
     int32_t n_members;
     int32_t n_groups;
     int32_t max_clique;
+    int32_t max_clique_res;
     const int32_t *clique_ptr;
     const int32_t *member_row;
     const int32_t *member_group;

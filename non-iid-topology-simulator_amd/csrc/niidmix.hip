@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -165,23 +166,27 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
 }
 
 // ----------------------------------------------------------------------------------------------
-// Clique-factored mixing (fast mode).  Work item = (clique, 256-column chunk); 8 waves; wave w holds
-// members w, w+8, w+16, ... (RPW rows per wave, float4 per lane per row) in registers.
-//   1. every member row is loaded once (all loads issued before the first use),
-//   2. per-wave partial group sums -> LDS -> every wave forms the full clique group sums S_g,
-//   3. y_m = a_m x_m + sum_g c_{m,g} S_g + residual terms (gateway edges), stored once.
-// Work order is XCD-aware (cliques of one chunk are consecutive on one XCD) so the residual rows a
-// gateway gathers from another clique are usually still in that XCD's L2.
-constexpr int kCliqueWaves = 8;
-
-template <int RPW, int G>
-__global__ __launch_bounds__(512) void k_mix_clique(
+// Clique-factored mixing (fast mode).  Work item = (clique, 256-column chunk); WAVES waves; wave w
+// holds members w, w+WAVES, w+2*WAVES, ... (RPW rows per wave, one float4 per lane per row) in
+// registers.
+//   0. lane r of each wave fetches the descriptor of the wave's r-th member (row, group,
+//      coefficients, residual range) with ONE vector load per field; v_readlane hands them to the
+//      scalar unit, so the RPW row loads issue back to back with no scalar-load round trips,
+//   1. every member row is loaded once from HBM (all loads in flight before the first use),
+//   2. per-wave partial group sums -> LDS; waves 0..G-1 each reduce one group -> LDS,
+//   3. y_m = a_m x_m + sum_g c_{m,g} S_g + residual terms (gateway edges), stored once (nt).
+// Work order is XCD-aware (the cliques of one chunk run back to back on one XCD) so the residual
+// rows a gateway gathers from another clique are normally still in that XCD's L2.
+template <int WAVES, int RPW, int G, int OCC, int RW, bool ONEBAR>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
-    __shared__ float4 red[G][kCliqueWaves][kWave];
+    static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
+    __shared__ float4 red[G][WAVES][kWave];
+    __shared__ float4 tot[ONEBAR ? 1 : G][kWave];
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
     for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
@@ -195,68 +200,143 @@ __global__ __launch_bounds__(512) void k_mix_clique(
         const int32_t m0 = clique_ptr[cq];
         const int32_t M = valid_chunk ? clique_ptr[cq + 1] - m0 : 0;
 
+        // 0. descriptors, one member per lane (lanes >= RPW idle)
+        const int kd = wave + WAVES * lane;
+        const bool dl = lane < RPW && kd < M;
+        int d_row = 0, d_grp = 0, d_rb = 0, d_re = 0;
+        float d_cf[1 + G];
+#pragma unroll
+        for (int g = 0; g <= G; ++g) d_cf[g] = 0.f;
+        if (dl) {
+            const int32_t m = m0 + kd;
+            d_row = member_row[m];
+            d_grp = member_group[m];
+            d_rb = res_ptr[m];
+            d_re = res_ptr[m + 1];
+#pragma unroll
+            for (int g = 0; g <= G; ++g) d_cf[g] = coef[(int64_t)m * (1 + G) + g];
+        }
+        // residual entries of this wave's members, in member-slot order: lane j < RW holds the
+        // j-th one (its source row and weight) so those rows load with the members, not after.
+        int d_rsrc = 0;
+        float d_rw = 0.f;
+        if (RW > 0) {
+            int pre = 0, q_j = -1;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int rb = __builtin_amdgcn_readlane(d_rb, r);
+                const int cnt = __builtin_amdgcn_readlane(d_re, r) - rb;
+                if (lane >= pre && lane < pre + cnt) q_j = rb + lane - pre;
+                pre += cnt;
+            }
+            if (lane < RW && q_j >= 0) {
+                d_rsrc = res_col[q_j];
+                d_rw = res_val[q_j];
+            } else {
+                d_rsrc = __builtin_amdgcn_readlane(d_row, 0);
+            }
+        }
+
+        // 1. member rows (and prefetched residual rows) -> registers
+        const float *xc = x + chunk * kChunk;
+        float *yc = y + chunk * kChunk;
+        const unsigned lo = 4u * (unsigned)lane;
         float4 v[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (wave + WAVES * r < M) {
+                const int64_t row = __builtin_amdgcn_readlane(d_row, r);
+                if (act) v[r] = ld4(xc + row * ld_x + lo);
+            }
+        }
+        float4 rv[RW > 0 ? RW : 1];
+#pragma unroll
+        for (int j = 0; j < RW; ++j) {
+            const int64_t row = __builtin_amdgcn_readlane(d_rsrc, j);
+            rv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (M > 0 && act) rv[j] = ld4(xc + row * ld_x + lo);
+        }
+        // 2. group sums
         float4 s[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) s[g] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
-            const int k = wave + kCliqueWaves * r;
-            v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (k < M && act) v[r] = ld4(x + (int64_t)member_row[m0 + k] * ld_x + c);
-        }
+            if (wave + WAVES * r < M) {
+                const int gr = __builtin_amdgcn_readlane(d_grp, r);
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int k = wave + kCliqueWaves * r;
-            if (k < M) {
-                const int g = member_group[m0 + k];
-#pragma unroll
-                for (int gg = 0; gg < G; ++gg)
-                    if (g == gg) {
-                        s[gg].x += v[r].x; s[gg].y += v[r].y; s[gg].z += v[r].z; s[gg].w += v[r].w;
+                for (int g = 0; g < G; ++g)
+                    if (gr == g) {
+                        s[g].x += v[r].x; s[g].y += v[r].y; s[g].z += v[r].z; s[g].w += v[r].w;
                     }
             }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
         __syncthreads();
+        if constexpr (ONEBAR) {
+            // every wave sums the partials itself: one barrier, more LDS reads
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float4 a = red[g][0][lane];
-#pragma unroll
-            for (int w = 1; w < kCliqueWaves; ++w) {
-                const float4 b = red[g][w][lane];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            for (int g = 0; g < G; ++g) {
+                float4 a = red[g][0][lane];
+#pragma unroll 4
+                for (int w = 1; w < WAVES; ++w) {
+                    const float4 b = red[g][w][lane];
+                    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+                }
+                s[g] = a;
             }
-            s[g] = a;
+            __syncthreads();   // red[] is rewritten by the next work item
+        } else {
+            if (wave < G) {
+                float4 a = red[wave][0][lane];
+#pragma unroll 4
+                for (int w = 1; w < WAVES; ++w) {
+                    const float4 b = red[wave][w][lane];
+                    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+                }
+                tot[wave][lane] = a;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int g = 0; g < G; ++g) s[g] = tot[g][lane];
         }
+        // 3. outputs
+        int pre = 0;
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
-            const int k = wave + kCliqueWaves * r;
-            if (k < M) {
-                const int32_t m = m0 + k;
-                const float *cf = coef + (int64_t)m * (1 + G);
-                const float a = cf[0];
-                float4 o = make_float4(a * v[r].x, a * v[r].y, a * v[r].z, a * v[r].w);
+            if (wave + WAVES * r < M) {
+                const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_cf[0]), r));
+                float4 o = make_float4(af * v[r].x, af * v[r].y, af * v[r].z, af * v[r].w);
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const float cg = cf[1 + g];
+                    const float cg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_cf[1 + g]), r));
                     o.x = __builtin_fmaf(cg, s[g].x, o.x);
                     o.y = __builtin_fmaf(cg, s[g].y, o.y);
                     o.z = __builtin_fmaf(cg, s[g].z, o.z);
                     o.w = __builtin_fmaf(cg, s[g].w, o.w);
                 }
-                const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
-                if (act) {
-                    for (int32_t q = rb; q < re; ++q) {
-                        const float4 xr = ld4(x + (int64_t)res_col[q] * ld_x + c);
+                const int32_t rb = __builtin_amdgcn_readlane(d_rb, r);
+                const int32_t re = __builtin_amdgcn_readlane(d_re, r);
+                const int64_t row = __builtin_amdgcn_readlane(d_row, r);
+                if (rb < re) {
+                    // entries [pre, pre + re - rb) of this wave's residual list
+#pragma unroll
+                    for (int j = 0; j < RW; ++j)
+                        if (j >= pre && j < pre + (re - rb)) {
+                            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_rw), j));
+                            o = axpy4<false>(w, rv[j], o);
+                        }
+                    for (int32_t q = rb + (RW > pre ? RW - pre : 0); q < re; ++q) {   // beyond the prefetch
+                        const float4 xr = act ? ld4(xc + (int64_t)res_col[q] * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
                         o = axpy4<false>(res_val[q], xr, o);
                     }
-                    st4_nt(y + (int64_t)member_row[m] * ld_y + c, o);
+                    pre += re - rb;
                 }
+                if (act) st4_nt(yc + row * ld_y + lo, o);
             }
         }
-        __syncthreads();  // red[] is reused by the next work item
     }
 }
 
@@ -406,26 +486,56 @@ bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) 
     return a < b + b_elems && b < a + a_elems;
 }
 
-template <int RPW, int G>
+template <int WAVES, int RPW, int G, int OCC, int RW, bool ONEBAR>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     const int64_t grid = grid_for(n_items);
-    hipLaunchKernelGGL((k_mix_clique<RPW, G>), dim3((unsigned)grid), dim3(512), 0, s, x, ld_x, y,
-                       ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group,
-                       pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_items);
+    hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, ONEBAR>), dim3((unsigned)grid),
+                       dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
+                       pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
+                       pl->res_val, n_items);
 }
 
-template <int RPW>
+template <int WAVES, int RPW, int OCC, int RW, bool ONEBAR>
 int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                     const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     switch (pl->n_groups) {
-        case 1: launch_clique<RPW, 1>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 2: launch_clique<RPW, 2>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 3: launch_clique<RPW, 3>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 4: launch_clique<RPW, 4>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, ONEBAR>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, ONEBAR>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, ONEBAR>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, ONEBAR>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
     return check_launch("k_mix_clique");
+}
+
+// Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
+// targets, RW = residual rows prefetched per wave, ONEBAR = single-barrier reduction.
+// NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<onebar> overrides the choice (tuning only).
+int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                        const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
+    int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0;
+    if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob);
+    const int mc = pl->max_clique;
+    if (waves * rpw < mc) {
+        rw = 2; ob = 0;
+        if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
+        else if (mc <= 32) { waves = 8; rpw = 4; occ = 8; }
+        else if (mc <= 64) { waves = 16; rpw = 4; occ = 8; }
+        else if (mc <= 104) { waves = 8; rpw = 13; occ = 4; }
+        else if (mc <= 128) { waves = 16; rpw = 8; occ = 4; }
+        else if (mc <= 256) { waves = 16; rpw = 16; occ = 4; }
+        else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
+    }
+#define NIIDMIX_TILE(W, R, O, RWV, OB) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB) return launch_clique_g<W, R, O, RWV, OB>(x, ld_x, y, ld_y, p, pl, n_items, s)
+    NIIDMIX_TILE(8, 2, 8, 2, 0); NIIDMIX_TILE(8, 4, 8, 2, 0); NIIDMIX_TILE(16, 4, 8, 2, 0);
+    NIIDMIX_TILE(8, 13, 4, 2, 0); NIIDMIX_TILE(16, 8, 4, 2, 0); NIIDMIX_TILE(16, 16, 4, 2, 0);
+    // tuning alternatives (NIIDMIX_CLIQUE_TILE)
+    NIIDMIX_TILE(8, 13, 4, 0, 0); NIIDMIX_TILE(8, 13, 4, 2, 1); NIIDMIX_TILE(8, 13, 4, 4, 0);
+    NIIDMIX_TILE(16, 7, 8, 0, 0); NIIDMIX_TILE(16, 7, 8, 2, 0); NIIDMIX_TILE(16, 7, 8, 2, 1);
+    NIIDMIX_TILE(16, 7, 4, 2, 0);
+#undef NIIDMIX_TILE
+    return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%d", waves, rpw, occ, rw, ob);
 }
 
 }  // namespace
@@ -475,18 +585,15 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
     if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
-    if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))
-        return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
+    if (plan->max_clique > 256)
+        return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", plan->max_clique);
+    if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t n_chunks = (p + kChunk - 1) / kChunk;
     const int64_t n_items = (int64_t)plan->n_cliques * ((n_chunks + 7) / 8) * 8;
-    const int mc = plan->max_clique;
-    if (mc <= 16) return launch_clique_g<2>(x, ld_x, y, ld_y, p, plan, n_items, s);
-    if (mc <= 32) return launch_clique_g<4>(x, ld_x, y, ld_y, p, plan, n_items, s);
-    if (mc <= 64) return launch_clique_g<8>(x, ld_x, y, ld_y, p, plan, n_items, s);
-    if (mc <= 128) return launch_clique_g<16>(x, ld_x, y, ld_y, p, plan, n_items, s);
-    if (mc <= 256) return launch_clique_g<32>(x, ld_x, y, ld_y, p, plan, n_items, s);
-    return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
+    if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))
+        return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
+    return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, n_items, s);
 }
 
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,

@@ -25,7 +25,7 @@ _i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
 class CliquePlanC(ctypes.Structure):
     """Mirror of struct niidmix_clique_plan (include/niidmix.h)."""
     _fields_ = [("n_cliques", _i32), ("n_members", _i32), ("n_groups", _i32), ("max_clique", _i32),
-                ("clique_ptr", _vp), ("member_row", _vp), ("member_group", _vp), ("coef", _vp),
+                ("max_clique_res", _i32), ("clique_ptr", _vp), ("member_row", _vp), ("member_group", _vp), ("coef", _vp),
                 ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp)]
 
 

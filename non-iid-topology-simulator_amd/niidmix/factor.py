@@ -23,7 +23,8 @@ from dataclasses import dataclass
 import numpy as np
 
 MAX_GROUPS = 4          # template limit of k_mix_clique
-MAX_CLIQUE = 256        # 8 waves x 32 register rows
+MAX_CLIQUE = 256        # register rows of k_mix_clique_wave (one lane per column)
+MAX_CLIQUE_RES = 64     # residual source rows prefetched per clique (16 when a clique > 128)
 
 
 @dataclass
@@ -31,6 +32,7 @@ class CliquePlan:
     n: int
     n_groups: int
     max_clique: int
+    max_clique_res: int
     clique_ptr: np.ndarray     # int32 [C+1]
     member_row: np.ndarray     # int32 [M]
     member_group: np.ndarray   # int32 [M]
@@ -179,7 +181,13 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
     n_res = int(res_ptr[-1])
     if n_res > max_res_per_node * n:
         return None, f"{n_res} residual terms > {max_res_per_node} per node"
-    plan = CliquePlan(n=n, n_groups=G, max_clique=biggest, clique_ptr=clique_ptr,
+    per_clique = res_ptr[clique_ptr[1:]] - res_ptr[clique_ptr[:-1]]
+    max_cr = int(per_clique.max()) if len(per_clique) else 0
+    cap = MAX_CLIQUE_RES if biggest <= 128 else 16
+    if max_cr > cap:
+        return None, f"a clique has {max_cr} residual terms > {cap}"
+    plan = CliquePlan(n=n, n_groups=G, max_clique=biggest, max_clique_res=max_cr,
+                      clique_ptr=clique_ptr,
                       member_row=member_row, member_group=member_group, coef=coef,
                       res_ptr=res_ptr.astype(np.int32),
                       res_col=np.asarray(res_cols, np.int32),

@@ -3,7 +3,7 @@
 Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
   mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, out,
-             max_clique)                            k_mix_clique (fast, HBM-bound)
+             max_clique, max_clique_res)            k_mix_clique_wave (fast, HBM-bound)
   mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
 All ops launch on torch's current HIP stream of the input's device, never synchronise, and raise
@@ -89,7 +89,7 @@ def mix_csr(x: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor, val: torc
 def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
                member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
                res_col: torch.Tensor, res_val: torch.Tensor, out: torch.Tensor,
-               max_clique: int) -> None:
+               max_clique: int, max_clique_res: int) -> None:
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -105,7 +105,8 @@ def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tens
     _vec("res_col", res_col, torch.int32, dev)
     _vec("res_val", res_val, torch.float32, dev, res_col.numel())
     _no_overlap(x, out)
-    plan = _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), clique_ptr.data_ptr(),
+    plan = _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), int(max_clique_res),
+                            clique_ptr.data_ptr(),
                             member_row.data_ptr(), member_group.data_ptr(), coef.data_ptr(),
                             res_ptr.data_ptr(), res_col.data_ptr() if res_col.numel() else
                             res_ptr.data_ptr(), res_val.data_ptr() if res_val.numel() else
@@ -183,7 +184,7 @@ class Mixer:
     def kernel_for(self, mode="fast", x=None):
         if mode == "exact":
             return "csr-exact"
-        if self.plan is not None and (x is None or (x.shape[1] % 4 == 0 and _ld(x) % 4 == 0)):
+        if self.plan is not None:
             return "clique"
         if self.dense:
             return "dense"
@@ -200,7 +201,8 @@ class Mixer:
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
-                       self.p_res_ptr, self.p_res_col, self.p_res_val, out, self.plan.max_clique)
+                       self.p_res_ptr, self.p_res_col, self.p_res_val, out, self.plan.max_clique,
+                       self.plan.max_clique_res)
         elif k == "dense":
             w = self.w_dense if self.w_dense is not None else \
                 torch.from_numpy(self.csr.dense()).to(x.device)
