@@ -126,6 +126,13 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
 int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, float *mean,
                           double *dist2, int mode, void *stream);
 
+/* Strided host <-> device copy (hipMemcpy2DAsync) of `rows` rows of `width_bytes` each, used by
+ * the host-resident drop-in (niidmix.slab) to stream column windows of the pinned [N, P] host slab
+ * through HBM while the previous window is being mixed.  kind: 0 = host->device, 1 = device->host,
+ * 2 = device->device.  Stream-ordered; host memory must be pinned for the copy to be asynchronous. */
+int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,
+                         int64_t width_bytes, int64_t rows, int kind, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

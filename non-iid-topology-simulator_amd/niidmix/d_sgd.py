@@ -1,0 +1,293 @@
+#!/usr/bin/env python
+"""Drop-in D-SGD algorithm plugin whose per-round neighbour mixing runs on MI355X.
+
+Same plugin API as the reference module tools/simulate/algorithm/d_sgd.py, so tools/simulate/run.py
+(`algo = import_module(params['algorithm']['module'])`, run.py:50) and the tools/tests/*.sh
+pipelines use it unchanged once params.algorithm.module = 'niidmix.d_sgd':
+
+  optimizer(model, params)                  -> torch.optim.SGD            (d_sgd.py:118-122)
+  init(nodes, topology, params)             -> (state, 0, False)          (d_sgd.py:124-143)
+  next_step(state, params, rundir)          -> (state, losses, epoch_done, active_nodes)  (:178-254)
+  average(nodes, topology, params)          -> None, Jacobi mixing of every node's model  (:96-116)
+  update_models / average_gradients / update_gradients / gradient       (:19-94)
+
+Only average() changes implementation: the nodes' models become views of one pinned host slab
+(niidmix.slab.NodeSlab), each round streams that slab through HBM in column windows and the HIP
+kernels mix it (niidmix.ops.Mixer).  Mixing mode (params['algorithm']['mixing-mode'], or the
+NIIDMIX_MODE environment variable):
+  'exact' (default)  bit-identical to the reference loop (tests/test_gpu_dropin.py)
+  'fast'             clique-factored / MFMA kernels, within 1e-5 condition-aware relative
+Local training, gradient variants and sampling stay on the CPU exactly as in the reference.
+"""
+import argparse
+import itertools
+import json
+import logging
+import os
+from random import Random
+
+import torch
+import torch.nn.functional as F
+
+from . import meta as m
+from . import model as nm
+from .topology import load as load_topology, to_csr
+
+MODULE = "niidmix.d_sgd"
+
+
+# ------------------------------------------------------------------------------------------------
+# gradient helpers (CPU, as the reference)
+def average_gradients(models):
+    """Mean of the models' gradients (d_sgd.py:19-27): zeros, add every grad, divide by count."""
+    with torch.no_grad():
+        acc = [torch.zeros_like(q.grad.data) for q in models[0].parameters()]
+        for mdl in models:
+            for a, q in zip(acc, mdl.parameters()):
+                a.add_(q.grad.data)
+        for a in acc:
+            a.div_(len(models))
+        return acc
+
+
+def update_models(models, new_model):
+    """p.mul_(0.); p.add_(new_p) for every parameter (d_sgd.py:29-35)."""
+    with torch.no_grad():
+        for mdl in models:
+            for q, nq in zip(mdl.parameters(), new_model.parameters()):
+                q.mul_(0.)
+                q.add_(nq)
+    return models
+
+
+def update_gradients(models, gradients):
+    """Overwrite every model's gradients (d_sgd.py:37-45)."""
+    with torch.no_grad():
+        for mdl in models:
+            for g, q in zip(gradients, mdl.parameters()):
+                if q.grad is None:
+                    q.grad = torch.zeros_like(q)
+                q.grad.data.zero_()
+                q.grad.data.add_(g)
+    return models
+
+
+def gradient(nodes, topology, params):
+    """Apply the local, clique-averaged or unbiased gradient, then step (d_sgd.py:47-94)."""
+    alg = params["algorithm"]
+    if not alg["clique-gradient"] and not alg["unbiased-gradient"]:
+        for n in nodes:
+            n["optimizer"].step()
+        return
+    with torch.no_grad():
+        if alg["clique-gradient"]:
+            removed = params["topology"].get("remove-clique-edges", 0)
+            edges = topology["edges"]
+            for clique in topology["cliques"]:
+                if not removed:
+                    members = [nodes[r]["model"] for r in clique]
+                    update_gradients(members, average_gradients(members))
+                    for r in clique:
+                        nodes[r]["optimizer"].step()
+                else:
+                    grads = {}
+                    for r in clique:
+                        peers = [nodes[q]["model"] for q in clique if q == r or q in edges[r]]
+                        grads[r] = average_gradients(peers)
+                    for r in clique:
+                        update_gradients([nodes[r]["model"]], grads[r])
+                        nodes[r]["optimizer"].step()
+        elif alg["unbiased-gradient"]:
+            hoods = topology["neighbourhoods"]
+            grads = {n["rank"]: average_gradients([nodes[q]["model"] for q in hoods[n["rank"]]])
+                     for n in nodes}
+            for n in nodes:
+                update_gradients([n["model"]], grads[n["rank"]])
+                n["optimizer"].step()
+        else:
+            raise Exception("Invalid execution path, previous cases should cover all possibilities.")
+
+
+# ------------------------------------------------------------------------------------------------
+# the GPU mixing step
+class _Engine:
+    """NodeSlab + Mixer + SlabMixer for one (node list, topology) pair."""
+
+    def __init__(self, nodes, topology, device):
+        from .ops import Mixer
+        from .slab import NodeSlab, SlabMixer
+        self.topology = topology
+        self.weights_id = id(topology.get("weights"))
+        self.slab = NodeSlab([n["model"] for n in nodes])
+        csr = to_csr(topology)
+        if csr.n != self.slab.n:
+            raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=device)
+        self.runner = SlabMixer(self.mixer, self.slab.n, self.slab.p, device,
+                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 16)))
+
+    def valid_for(self, nodes, topology):
+        return (topology is self.topology and id(topology.get("weights")) == self.weights_id
+                and self.slab.owns([n["model"] for n in nodes]))
+
+
+_engines = {}
+
+
+def _mode(params):
+    mode = os.environ.get("NIIDMIX_MODE") or params.get("algorithm", {}).get("mixing-mode", "exact")
+    if mode not in ("exact", "fast"):
+        raise ValueError(f"unknown mixing mode {mode!r}")
+    return mode
+
+
+def average(nodes, topology, params):
+    """Every node's model <- sum_j W[j, rank] model_j over [self] + edges[rank], computed from the
+    pre-round models (Jacobi) then written back (update_models), as d_sgd.py:96-116 — one GPU pass
+    over the whole [N, P] slab instead of N*(deg+1)*n_tensors ATen calls."""
+    logging.info("  computing averages of models (GPU, %s)", _mode(params))
+    key = id(nodes)
+    eng = _engines.get(key)
+    if eng is None or not eng.valid_for(nodes, topology):
+        dev = torch.device("cuda", torch.cuda.current_device())
+        eng = _Engine(nodes, topology, dev)
+        _engines.clear()
+        _engines[key] = eng
+    eng.runner.mix(eng.slab.host, mode=_mode(params), timing=logging.getLogger().isEnabledFor(logging.INFO))
+    if eng.runner.last_timing:
+        logging.info("  mixing round: %s", eng.runner.last_timing)
+
+
+# ------------------------------------------------------------------------------------------------
+# plugin API
+def optimizer(model, params):
+    return torch.optim.SGD(model.parameters(), lr=params["algorithm"]["learning-rate"],
+                           momentum=params["algorithm"]["learning-momentum"])
+
+
+def _loader(node, params):
+    return iter(torch.utils.data.DataLoader(node["train-set"],
+                                            batch_size=int(params["algorithm"]["batch-size"]),
+                                            shuffle=True))
+
+
+def init(nodes, topology, params):
+    logging.basicConfig(level=getattr(logging, params["meta"]["log"].upper(), None))
+    state = {"nodes": nodes, "topology": topology, "step": 0}
+    for n in nodes:
+        n["train-iterator"] = _loader(n, params)
+    if params["algorithm"]["initial-averaging"]:
+        center = nm.average([nodes[r]["model"] for r in range(len(nodes))])
+        for r in range(len(nodes)):
+            update_models([nodes[r]["model"]], center)
+    return (state, 0, False)
+
+
+def _peek(iterator):
+    try:
+        first = next(iterator)
+    except StopIteration:
+        return None
+    return itertools.chain([first], iterator)
+
+
+_sample_cache = {}
+
+
+def get_sample(state, params, step):
+    """Active nodes of the 'sample' topology (d_sgd.py:157-175)."""
+    if step in _sample_cache:
+        return _sample_cache[step]
+    rnd = Random(42 + step)
+    method = params["topology"]["sample-method"]
+    size = params["topology"]["sample-size"]
+    if method == "random":
+        return rnd.sample(state["nodes"], size)
+    if method == "random-with-overlap":
+        if step == 0:
+            return rnd.sample(state["nodes"], size)
+        previous = get_sample(state, params, step - 1)
+        active = rnd.sample(previous, params["topology"]["sample-overlap"])
+        rest = [n for n in state["nodes"] if n not in active]
+        active += rnd.sample(rest, size - params["topology"]["sample-overlap"])
+        _sample_cache[step] = active
+        return active
+
+
+def next_step(state, params, rundir):
+    sample = params["topology"]["name"] == "sample"
+    active = get_sample(state, params, state["step"]) if sample else state["nodes"]
+    topology = state["topology"]
+    losses, epoch_done = {}, {}
+    for node in active:                                   # local training (CPU)
+        data, target = next(node["train-iterator"])
+        node["optimizer"].zero_grad()
+        loss = F.nll_loss(node["model"].forward(data, params), target)
+        loss.backward()
+        losses[node["rank"]] = loss.tolist()
+        rest = _peek(node["train-iterator"])
+        done = rest is None
+        if done:
+            node["epoch"] += 1
+            node["train-iterator"] = _loader(node, params)
+        else:
+            node["train-iterator"] = rest
+        epoch_done[node["rank"]] = done
+    if not sample:
+        gradient(active, topology, params)
+        average(active, topology, params)                 # ★ GPU
+        if params["topology"]["name"] == "random-graph" and params["topology"]["randomize"]:
+            params["topology"]["topology-seed"] += 1
+            from setup.topology.random_graph import generate_topology   # reference generator
+            fresh = generate_topology(state["nodes"], params)
+            with open(os.path.join(rundir, "topology.json"), "w+") as f:
+                json.dump(fresh, f)
+            fresh["edges"] = {int(r): fresh["edges"][r] for r in fresh["edges"]}
+            fresh["weights"] = torch.tensor(fresh["weights"])
+            state["topology"] = fresh
+    else:
+        for n in active:
+            n["optimizer"].step()
+        center = nm.average([n["model"] for n in active],
+                            [1 / len(active) for _ in active])
+        update_models([n["model"] for n in state["nodes"]], center)
+    state["step"] += 1
+    return state, losses, epoch_done, active
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Provide Options for D-SGD (MI355X mixing).")
+    ap.add_argument("--rundir", type=str, default=None)
+    ap.add_argument("--learning-rate", type=float, default=0.1)
+    ap.add_argument("--learning-momentum", type=float, default=0.0)
+    ap.add_argument("--batch-size", type=int, default=128)
+    ap.add_argument("--initial-averaging", action="store_const", const=True, default=False)
+    ap.add_argument("--clique-gradient", action="store_const", const=True, default=False)
+    ap.add_argument("--unbiased-gradient", action="store_const", const=True, default=False)
+    ap.add_argument("--mixing-mode", choices=["exact", "fast"], default="exact",
+                    help="exact: bit-identical to the reference loop; fast: clique/MFMA kernels")
+    args = ap.parse_args(argv)
+    rundir = m.rundir(args)
+    params = m.params(rundir)
+    topology = load_topology(rundir)
+    if args.clique_gradient:
+        assert "cliques" in topology, \
+            "Invalid --clique-gradient with {} topology, no 'cliques' found in topology.json.".format(
+                params["topology"]["name"])
+    if args.unbiased_gradient:
+        assert "neighbourhoods" in topology, \
+            "Invalid --unbiased-gradient with {} topology, no 'neighbourhoods' found in topology.json.".format(
+                params["topology"]["name"])
+    m.extend(rundir, "algorithm", {
+        "name": "d-sgd", "module": MODULE,
+        "learning-rate": args.learning_rate, "learning-momentum": args.learning_momentum,
+        "batch-size": args.batch_size, "initial-averaging": args.initial_averaging,
+        "clique-gradient": args.clique_gradient, "unbiased-gradient": args.unbiased_gradient,
+        "mixing-mode": args.mixing_mode,
+    })
+    if args.rundir is None:
+        print(rundir)
+
+
+if __name__ == "__main__":
+    main()

@@ -181,10 +181,10 @@ class Mixer:
         self.dense = csr.nnz >= dense_threshold * self.n * self.n and self.n >= 64
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
 
-    def kernel_for(self, mode="fast", x=None):
+    def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
             return "csr-exact"
-        if self.plan is not None:
+        if self.plan is not None and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:
             return "dense"
@@ -193,7 +193,7 @@ class Mixer:
     def __call__(self, x, out=None, mode="fast", kernel=None):
         if out is None:
             out = torch.empty((self.n, x.shape[1]), dtype=torch.float32, device=x.device)
-        k = kernel or self.kernel_for(mode, x)
+        k = kernel or self.kernel_for(mode, x, out)
         if k == "csr-exact":
             mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT)
         elif k == "csr-fast":
@@ -210,6 +210,11 @@ class Mixer:
         else:
             raise ValueError(f"unknown kernel {k!r}")
         return out
+
+
+def _clique_ok(x):
+    """k_mix_clique streams float4 columns: p and ld multiples of 4, 16-B aligned base."""
+    return x.shape[1] % 4 == 0 and _ld(x) % 4 == 0 and x.data_ptr() % 16 == 0
 
 
 def csr_from_numpy(row_ptr, col, val):

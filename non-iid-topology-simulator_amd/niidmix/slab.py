@@ -1,0 +1,138 @@
+"""Host-resident node state for the drop-in.
+
+The reference keeps every simulated node's model as its own nn.Module on the host between rounds
+(training runs on CPU, d_sgd.py:186-213).  NodeSlab re-points the parameters of N identical models
+at views of ONE pinned host slab [N, P] (row = node, flattened in model.parameters() order), so the
+per-round mixing needs no gather/scatter: the slab streams to HBM, is mixed there by the HIP
+kernels, and streams back.  Training, optimizers (the Parameter objects are unchanged, only their
+.data) and the logger keep working on the models as before.
+
+SlabMixer pipelines one round over column windows of the slab (columns are independent in Θ' = Wᵀ Θ):
+    H2D window k+1  ||  mix window k  ||  D2H window k-1
+on three HIP streams, so the round costs ~max(H2D, D2H) on PCIe rather than their sum.  The copies
+are strided 2-D memcpys straight from/to the pinned slab (niidmix_copy2d_async).  Jacobi holds:
+window k's inputs are on the device before its outputs are written back, and windows never share
+columns.
+"""
+import ctypes
+import time
+
+import torch
+
+from . import _lib
+
+
+def _flat_shapes(model):
+    return [(p.shape, p.numel()) for p in model.parameters()]
+
+
+class NodeSlab:
+    """Parameters of `models` as views into one fp32 [N, P] host slab (pinned by default)."""
+
+    def __init__(self, models, pin=True):
+        models = list(models)
+        if not models:
+            raise ValueError("NodeSlab needs at least one model")
+        shapes = _flat_shapes(models[0])
+        for m in models:
+            if _flat_shapes(m) != shapes:
+                raise ValueError("all node models must have the same parameter shapes")
+            for q in m.parameters():
+                if q.dtype != torch.float32:
+                    raise ValueError("the mixing kernels are fp32; got a %s parameter" % q.dtype)
+        self.models = models
+        self.shapes = shapes
+        self.n = len(models)
+        self.p = sum(k for _, k in shapes)
+        pin = pin and torch.cuda.is_available()
+        self.host = torch.empty((self.n, self.p), dtype=torch.float32, pin_memory=pin)
+        with torch.no_grad():
+            for i, m in enumerate(models):
+                off = 0
+                for q, (shape, k) in zip(m.parameters(), shapes):
+                    view = self.host[i, off:off + k]
+                    view.copy_(q.detach().reshape(-1))
+                    q.data = view.view(shape)
+                    off += k
+
+    def owns(self, models):
+        """True iff `models` are exactly this slab's models, in order, still backed by it."""
+        if len(models) != self.n:
+            return False
+        base = self.host.data_ptr()
+        for i, m in enumerate(models):
+            if m is not self.models[i]:
+                return False
+            q = next(iter(m.parameters()), None)
+            if q is not None and q.data_ptr() != base + i * self.p * 4:
+                return False
+        return True
+
+
+def _copy2d(dst, dpitch, src, spitch, width, rows, kind, stream):
+    rc = _lib.lib.niidmix_copy2d_async(dst, dpitch, src, spitch, width, rows, kind,
+                                       ctypes.c_void_p(stream.cuda_stream))
+    _lib.check(rc, "niidmix_copy2d_async")
+
+
+class SlabMixer:
+    """One mixing round of a host [N, P] slab through the GPU, pipelined over column windows."""
+
+    def __init__(self, mixer, n, p, device, window=1 << 16):
+        self.mixer = mixer
+        self.n, self.p = n, p
+        self.device = torch.device(device)
+        self.window = max(256, (min(window, p) + 255) // 256 * 256)
+        w = self.window
+        self.dx = [torch.empty((n, w), dtype=torch.float32, device=self.device) for _ in range(2)]
+        self.dy = [torch.empty((n, w), dtype=torch.float32, device=self.device) for _ in range(2)]
+        self.s_h2d = torch.cuda.Stream(self.device)
+        self.s_mix = torch.cuda.Stream(self.device)
+        self.s_d2h = torch.cuda.Stream(self.device)
+        self.last_timing = None
+
+    def mix(self, host, mode="exact", kernel=None, timing=False):
+        """host: pinned fp32 [N, P] (may be any row-major slab with stride(1) == 1)."""
+        n, p, w = self.n, self.p, self.window
+        assert host.shape == (n, p) and host.dtype == torch.float32 and host.stride(1) == 1
+        ld_h = host.stride(0) * 4
+        base = host.data_ptr()
+        nwin = (p + w - 1) // w
+        ev_in = [torch.cuda.Event() for _ in range(nwin)]
+        ev_mix = [torch.cuda.Event() for _ in range(nwin)]
+        ev_out = [torch.cuda.Event() for _ in range(nwin)]
+        t_ev = None
+        if timing:
+            t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            t0 = time.perf_counter()
+            t_ev[0].record(self.s_h2d)
+        for k in range(nwin):
+            c0 = k * w
+            cw = min(w, p - c0)
+            buf = k % 2
+            with torch.cuda.stream(self.s_h2d):
+                if k >= 2:
+                    self.s_h2d.wait_event(ev_mix[k - 2])          # dx[buf] consumed
+                _copy2d(self.dx[buf].data_ptr(), w * 4, base + c0 * 4, ld_h, cw * 4, n, 0,
+                        self.s_h2d)
+                ev_in[k].record(self.s_h2d)
+            with torch.cuda.stream(self.s_mix):
+                self.s_mix.wait_event(ev_in[k])
+                if k >= 2:
+                    self.s_mix.wait_event(ev_out[k - 2])          # dy[buf] drained
+                self.mixer(self.dx[buf][:, :cw], out=self.dy[buf][:, :cw], mode=mode,
+                           kernel=kernel)
+                ev_mix[k].record(self.s_mix)
+            with torch.cuda.stream(self.s_d2h):
+                self.s_d2h.wait_event(ev_mix[k])
+                _copy2d(base + c0 * 4, ld_h, self.dy[buf].data_ptr(), w * 4, cw * 4, n, 1,
+                        self.s_d2h)
+                ev_out[k].record(self.s_d2h)
+        if timing:
+            t_ev[1].record(self.s_d2h)
+        self.s_d2h.synchronize()
+        if timing:
+            self.last_timing = {"round_s": time.perf_counter() - t0,
+                                "gpu_span_s": t_ev[0].elapsed_time(t_ev[1]) / 1e3,
+                                "windows": nwin, "window_cols": w}
+        return host

@@ -1,0 +1,158 @@
+"""The drop-in plugin (niidmix.d_sgd / niidmix.model) on the GPU against the reference's golden
+vectors: same call signatures as tools/simulate/algorithm/d_sgd.py and tools/setup/model, same bits."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_cases, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+class FlatModel(torch.nn.Module):
+    def __init__(self, shapes):
+        super().__init__()
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(s)) for s in shapes])
+
+
+def _nodes_and_topology(g):
+    shapes = [tuple(s) for s in json.loads(str(g["shapes_json"]))]
+    n = len(g["row_ptr"]) - 1
+    W = torch.zeros(n, n)
+    edges = {}
+    for i in range(n):
+        b, e = g["row_ptr"][i], g["row_ptr"][i + 1]
+        edges[i] = g["col"][b + 1:e].tolist()
+        W[torch.from_numpy(g["col"][b:e].astype(np.int64)), i] = torch.from_numpy(g["val"][b:e])
+    nodes = []
+    for i in range(n):
+        m = FlatModel(shapes)
+        off = 0
+        with torch.no_grad():
+            for q in m.parameters():
+                k = q.numel()
+                q.copy_(torch.from_numpy(g["x"][i, off:off + k].copy()).view_as(q))
+                off += k
+        nodes.append({"rank": i, "model": m})
+    topo = {"edges": edges, "weights": W}
+    if "cliques" in g:
+        topo["cliques"] = g["cliques"]
+    return nodes, topo
+
+
+def _params_of(nodes):
+    return np.stack([torch.cat([q.detach().reshape(-1) for q in nd["model"].parameters()]).numpy()
+                     for nd in nodes])
+
+
+@pytest.mark.parametrize("name", [n for n in golden_cases()])
+def test_dsgd_average_bitwise(name, gpu, oracle_mod, monkeypatch):
+    """niidmix.d_sgd.average(nodes, topology, params) == reference d_sgd.average, bit for bit,
+    on the reference's golden vectors; a second round equals the oracle applied twice."""
+    monkeypatch.setenv("NIIDMIX_WINDOW", "256")     # several column windows -> pipelined path
+    from niidmix import d_sgd
+    g = load_golden(name)
+    nodes, topo = _nodes_and_topology(g)
+    d_sgd.average(nodes, topo, {})
+    y1 = _params_of(nodes)
+    assert oracle_mod.bitwise_equal(y1, g["y"]), name
+    d_sgd.average(nodes, topo, {})
+    y2 = _params_of(nodes)
+    ref2 = oracle_mod.mix_exact_c(g["y"], g["row_ptr"], g["col"], g["val"])
+    assert oracle_mod.bitwise_equal(y2, ref2), name
+
+
+def test_dsgd_average_fast_mode(gpu, oracle_mod, monkeypatch):
+    monkeypatch.setenv("NIIDMIX_MODE", "fast")
+    from niidmix import d_sgd
+    g = load_golden("dcliques1000_fc_p64")
+    nodes, topo = _nodes_and_topology(g)
+    d_sgd.average(nodes, topo, {})
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(_params_of(nodes), g["y"], bound, rtol=1e-5)
+    assert ok, worst
+
+
+def test_model_average_uniform_and_weighted(gpu):
+    from niidmix import model as nm
+    d = np.load(__import__("conftest").GOLDEN + "/uniform_avg_k7_p100.npz")
+    models = []
+    for k in range(d["x"].shape[0]):
+        m = FlatModel([(100,)])
+        with torch.no_grad():
+            m.ps[0].copy_(torch.from_numpy(d["x"][k]))
+        models.append(m)
+    c = nm.average(models)
+    assert np.array_equal(c.ps[0].detach().numpy().view(np.uint32), d["y"][0].view(np.uint32))
+    # weighted with 0-d fp32 tensors, as d_sgd passes W[src, rank]
+    w = [torch.tensor(0.25), torch.tensor(0.5), torch.tensor(0.25)]
+    c = nm.average(models[:3], w)
+    x = d["x"][:3]
+    acc = x[0] * np.float32(0)
+    for k in range(3):
+        acc = acc + np.float32(w[k].item()) * x[k]
+    assert np.array_equal(c.ps[0].detach().numpy().view(np.uint32), acc.view(np.uint32))
+
+
+def test_consensus_distance(gpu):
+    from niidmix import model as nm
+    torch.manual_seed(0)
+    models = [torch.nn.Linear(30, 10) for _ in range(9)]
+    center, dist, norm = nm.consensus_distance(models)
+    flat = torch.stack([torch.cat([q.detach().reshape(-1) for q in m.parameters()]) for m in models]).double()
+    mean = flat.mean(0)
+    ref = torch.sqrt(((flat - mean) ** 2).sum(1))
+    np.testing.assert_allclose(dist, ref.numpy(), rtol=1e-6)
+    np.testing.assert_allclose(norm, float(torch.sqrt((mean ** 2).sum())), rtol=1e-6)
+
+
+def test_training_rounds_match_reference_loop(gpu, oracle_mod):
+    """A few D-SGD rounds (local SGD on CPU + mixing) of the tools/tests/basic.sh shape (2-node ring,
+    linear MNIST-shaped model, batch 125) with synthetic data: the GPU drop-in's parameters equal,
+    bit for bit, those of the same rounds with the reference loop (oracle) doing the mixing."""
+    from niidmix import d_sgd
+
+    def run(mix):
+        torch.manual_seed(1337)
+        params = {"meta": {"log": "WARNING", "seed": 1337},
+                  "model": {"input-size": 784},
+                  "topology": {"name": "ring"},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 125,
+                                "initial-averaging": True, "clique-gradient": False,
+                                "unbiased-gradient": False}}
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc = torch.nn.Linear(784, 10)
+
+            def forward(self, x, params):
+                return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+        g = torch.Generator().manual_seed(7)
+        data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+                for _ in range(1000)]
+        nodes = []
+        for r in range(2):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 500:(r + 1) * 500],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        topo = {"edges": {0: [1], 1: [0]}, "weights": torch.tensor([[0.5, 0.5], [0.5, 0.5]])}
+        orig = d_sgd.average
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for _ in range(6):
+                state, losses, done, active = d_sgd.next_step(state, params, None)
+        finally:
+            d_sgd.average = orig
+        return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
+                for n in nodes]
+
+    a = run("gpu")
+    b = run("oracle")
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)

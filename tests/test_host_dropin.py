@@ -1,0 +1,52 @@
+"""Drop-in host logic on CPU: NodeSlab views, meta/CLI registration."""
+import json
+import os
+import sys
+
+import torch
+
+from niidmix import meta
+from niidmix.slab import NodeSlab
+
+
+def test_nodeslab_views_and_optimizer():
+    torch.manual_seed(0)
+    models = [torch.nn.Linear(7, 3) for _ in range(4)]
+    before = [torch.cat([q.detach().reshape(-1).clone() for q in mm.parameters()]) for mm in models]
+    opts = [torch.optim.SGD(mm.parameters(), lr=0.1) for mm in models]
+    slab = NodeSlab(models, pin=False)
+    assert slab.host.shape == (4, 7 * 3 + 3)
+    for i in range(4):
+        assert torch.equal(slab.host[i], before[i])
+    # optimizer steps write straight into the slab
+    x = torch.randn(5, 7)
+    models[2](x).sum().backward()
+    opts[2].step()
+    flat = torch.cat([q.detach().reshape(-1) for q in models[2].parameters()])
+    assert torch.equal(slab.host[2], flat)
+    assert not torch.equal(slab.host[2], before[2])
+    assert slab.owns(models) and not slab.owns(models[::-1])
+
+
+def test_meta_extend_refuses_overwrite(tmp_path):
+    d = str(tmp_path)
+    meta.extend(d, "meta", {"seed": 1})
+    assert meta.params(d, "meta") == {"seed": 1}
+    try:
+        meta.extend(d, "meta", {"seed": 2})
+        raise RuntimeError("should have refused")
+    except AssertionError:
+        pass
+
+
+def test_cli_registers_plugin(tmp_path):
+    d = str(tmp_path)
+    topo = {"edges": {"0": [1], "1": [0]}, "weights": [[0.5, 0.5], [0.5, 0.5]]}
+    with open(os.path.join(d, "topology.json"), "w") as f:
+        json.dump(topo, f)
+    meta.extend(d, "topology", {"name": "ring"})
+    from niidmix import d_sgd
+    d_sgd.main(["--rundir", d, "--batch-size", "125"])
+    alg = meta.params(d, "algorithm")
+    assert alg["module"] == "niidmix.d_sgd" and alg["batch-size"] == 125
+    assert alg["mixing-mode"] == "exact"

@@ -24,6 +24,25 @@ __global__ void copy_lin_nt(const float4 *__restrict__ x, float4 *__restrict__ y
         __builtin_nontemporal_store(w, (f4 *)(y + i));
     }
 }
+__global__ void copy_lin_ntnt(const float4 *__restrict__ x, float4 *__restrict__ y, size_t n) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        f4 w = __builtin_nontemporal_load((const f4 *)(x + i));
+        __builtin_nontemporal_store(w, (f4 *)(y + i));
+    }
+}
+// 2 float4 per thread per iteration, loads first
+__global__ void copy_lin2_nt(const float4 *__restrict__ x, float4 *__restrict__ y, size_t n) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+        f4 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i + u * stride < n) w[u] = *(const f4 *)(x + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i + u * stride < n) __builtin_nontemporal_store(w[u], (f4 *)(y + i + u * stride));
+    }
+}
 __global__ void read_lin(const float4 *__restrict__ x, float *__restrict__ out, size_t n) {
     float s = 0.f;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -132,6 +151,9 @@ int main(int argc, char **argv) {
         snprintf(nm, 64, "copy_lin_nt g%d", grid);
         timeit(nm, 2.0 * bytes, [&] { copy_lin_nt<<<grid, 256>>>((const float4 *)x, (float4 *)y, n4); });
     }
+    timeit("copy_lin_ntnt g65536", 2.0 * bytes, [&] { copy_lin_ntnt<<<65536, 256>>>((const float4 *)x, (float4 *)y, n4); });
+    timeit("copy_lin2_nt g16384", 2.0 * bytes, [&] { copy_lin2_nt<<<16384, 256>>>((const float4 *)x, (float4 *)y, n4); });
+    timeit("copy_lin2_nt g4096", 2.0 * bytes, [&] { copy_lin2_nt<<<4096, 256>>>((const float4 *)x, (float4 *)y, n4); });
     timeit("read_lin g8192", 1.0 * bytes, [&] { read_lin<<<8192, 256>>>((const float4 *)x, o, n4); });
     timeit("write_lin g8192", 1.0 * bytes, [&] { write_lin<<<8192, 256>>>((float4 *)y, n4); });
     const int R = 100, C = (int)(N / R);
