@@ -53,11 +53,11 @@ class CliquePlan:
     def n_res(self):
         return len(self.res_col)
 
-    def effective_weights(self):
+    def effective_weights(self, n_in=None):
         """W_eff[src, dst] (float64) implied by the plan; equals W up to the fp32 rounding of a_i
         and of residual corrections."""
         n, G = self.n, self.n_groups
-        W = np.zeros((n, n), np.float64)
+        W = np.zeros((n_in or n, n), np.float64)
         for c in range(self.n_cliques):
             mem = self.member_row[self.clique_ptr[c]:self.clique_ptr[c + 1]]
             grp = self.member_group[self.clique_ptr[c]:self.clique_ptr[c + 1]]
@@ -118,8 +118,9 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
     if biggest > max_clique:
         return None, f"clique of {biggest} members > {max_clique}"
     deg = csr.degrees()
-    clique_of = np.empty(n, np.int64)
-    group_of = np.empty(n, np.int64)
+    n_in = max(csr.n_in, n)                 # a shard's CSR also reads halo rows >= n
+    clique_of = np.full(n_in, -1, np.int64)
+    group_of = np.full(n_in, -1, np.int64)
     groups_per_clique = []
     for ci, c in enumerate(cliques):
         c = np.asarray(c, np.int64)

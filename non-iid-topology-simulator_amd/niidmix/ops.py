@@ -178,7 +178,8 @@ class Mixer:
             self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
             self.p_res_col = torch.from_numpy(p.res_col).to(dev)
             self.p_res_val = torch.from_numpy(p.res_val).to(dev)
-        self.dense = csr.nnz >= dense_threshold * self.n * self.n and self.n >= 64
+        self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
+                      and self.n >= 64)
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
 
     def kernel_for(self, mode="fast", x=None, out=None):

@@ -57,10 +57,16 @@ def load(rundir):
 @dataclass
 class MixCSR:
     """CSR of W^T rows: row i lists (src, W[src, i]) with the node itself first, then edges[i] in
-    list order.  row_ptr int64 [N+1], col int32 [nnz], val fp32 [nnz]."""
+    list order.  row_ptr int64 [N+1], col int32 [nnz], val fp32 [nnz].  n_in (default N) is the
+    number of input rows the columns index: a node shard's CSR also reads halo rows >= N."""
     row_ptr: np.ndarray
     col: np.ndarray
     val: np.ndarray
+    n_in: int = None
+
+    def __post_init__(self):
+        if self.n_in is None:
+            self.n_in = len(self.row_ptr) - 1
 
     @property
     def n(self):
@@ -82,9 +88,9 @@ class MixCSR:
         return out
 
     def dense(self):
-        """W as the reference stores it: dense[src, dst] (fp32)."""
+        """W as the reference stores it: dense[src, dst] (fp32), [n_in, n]."""
         n = self.n
-        w = np.zeros((n, n), np.float32)
+        w = np.zeros((self.n_in, n), np.float32)
         dst = np.repeat(np.arange(n), np.diff(self.row_ptr))
         w[self.col, dst] = self.val
         return w
@@ -97,7 +103,7 @@ class MixCSR:
             raise ValueError("col/val length != row_ptr[-1]")
         if np.any(self.col[self.row_ptr[:-1]] != np.arange(n)):
             raise ValueError("first entry of row i must be i (the reference's models[0] = self)")
-        if self.nnz and (self.col.min() < 0 or self.col.max() >= n):
+        if self.nnz and (self.col.min() < 0 or self.col.max() >= self.n_in):
             raise ValueError("column index out of range")
         return self
 

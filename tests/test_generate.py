@@ -1,0 +1,23 @@
+"""The benchmark's D-Cliques generator restatement (niidmix.generate) reproduces the topologies the
+reference generators produced (golden fixtures): same cliques, same edge lists in the same order,
+same MH weights bit for bit."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from niidmix import generate
+
+
+@pytest.mark.parametrize("name,n,size,inter", [
+    ("dcliques1000_fc_p64", 1000, 100, "fully-connected"),
+    ("dcliques1000_smallworld_p16", 1000, 100, "smallworld"),
+    ("dcliques1000_ring_p16", 1000, 100, "ring"),
+    ("dcliques300_fc_p37", 300, 30, "fully-connected"),
+])
+def test_matches_reference_generator(name, n, size, inter):
+    g = load_golden(name)
+    csr, cliques = generate.dcliques_csr(n, size, inter, seed=1337)
+    assert cliques == g["cliques"]
+    np.testing.assert_array_equal(csr.row_ptr, g["row_ptr"])
+    np.testing.assert_array_equal(csr.col, g["col"])
+    assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))

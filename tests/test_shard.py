@@ -1,0 +1,117 @@
+"""Multi-GPU sharding logic on CPU: the clique-aligned partition, halo plan and RCCL-style exchange
+(here over gloo, world size 2 and 4), with the oracle as each rank's local compute.  The sharded
+round must equal the single-process round bit for bit (same operand order per row)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_golden
+from niidmix.shard import ShardPlan, ShardedMixer, window_layout
+from niidmix.topology import MixCSR
+
+
+def _csr(g):
+    return MixCSR(g["row_ptr"], g["col"], g["val"]).validate()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_plan_partition_and_halo(world, oracle_mod):
+    g = load_golden("dcliques1000_fc_p64")
+    csr = _csr(g)
+    plan = ShardPlan(csr, g["cliques"], world)
+    seen = np.concatenate(plan.nodes_of)
+    assert sorted(seen.tolist()) == list(range(1000))
+    for r in range(world):
+        sh = plan.local(r)
+        # whole cliques only
+        assert sum(len(c) for c in sh.cliques) == sh.n_local
+        # halo rows are exactly the remote sources the local rows read
+        need = set()
+        for gid in sh.nodes:
+            need.update(int(c) for c in csr.col[csr.row_ptr[gid]:csr.row_ptr[gid + 1]]
+                        if plan.owner[c] != r)
+        assert set(sh.halo.tolist()) == need
+        # local mixing over [local | halo] rows == global mixing of those rows, bit for bit
+        x_in = g["x"][np.concatenate([sh.nodes, sh.halo]).astype(np.int64)]
+        y = oracle_mod.mix_exact_c(x_in, sh.csr.row_ptr, sh.csr.col, sh.csr.val)
+        assert oracle_mod.bitwise_equal(y, g["y"][sh.nodes])
+        # what r sends to q is what q expects, in q's halo order
+        for q, idx in sh.send.items():
+            hq = plan.local(q)
+            expect = hq.halo[hq.halo_owner == r]
+            np.testing.assert_array_equal(sh.nodes[idx], expect)
+
+
+def test_window_layout():
+    assert window_layout(1 << 20, 8) == (8, 131072)
+    k, w = window_layout(1000, 8)
+    assert k * w >= 1000 and w % 256 == 0 and (k - 1) * w < 1000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, p, rounds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        g = load_golden(name)
+        csr = _csr(g)
+
+        def compute(x2d, out2d, kernel=None, mode="exact"):
+            sh = sm.shard
+            out2d.copy_(torch.from_numpy(oracle.mix_exact_c(
+                x2d.contiguous().numpy(), sh.csr.row_ptr, sh.csr.col, sh.csr.val)))
+
+        sm = ShardedMixer(csr, g.get("cliques"), world, rank, "cpu", p, windows=3, compute=compute)
+        x = sm.empty().zero_()
+        gx = g["x"][:, :p]
+        for k in range(sm.k):
+            c0 = k * sm.w
+            cw = min(sm.w, p - c0)
+            x[k, :sm.n_local, :cw] = torch.from_numpy(gx[sm.shard.nodes, c0:c0 + cw])
+        out = sm.empty().zero_()
+        for _ in range(rounds):
+            sm(x, out)
+            x, out = out, x
+        res = np.concatenate([x[k, :sm.n_local, :min(sm.w, p - k * sm.w)].numpy()
+                              for k in range(sm.k)], axis=1)
+        q.put((rank, sm.shard.nodes, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name", [(2, "dcliques1000_fc_p64"), (2, "ring100_p257"),
+                                        (4, "dcliques300_fc_p37")])
+def test_gloo_sharded_rounds(world, name, oracle_mod):
+    g = load_golden(name)
+    p = min(g["x"].shape[1], 40)
+    rounds = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, p, rounds, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref = g["x"][:, :p].copy()
+    for _ in range(rounds):
+        ref = oracle_mod.mix_exact_c(ref, g["row_ptr"], g["col"], g["val"])
+    full = np.zeros_like(ref)
+    for rank, nodes, res in got:
+        full[nodes] = res
+    assert oracle_mod.bitwise_equal(full, ref)
