@@ -110,6 +110,30 @@ typedef struct niidmix_clique_plan {
 int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                            const niidmix_clique_plan *plan, void *stream);
 
+/* Block-staged CSR mixing, exact or fast: the same result as niidmix_mix_csr_f32 (bit for bit in
+ * NIIDMIX_MODE_EXACT: same per-row operand order and roundings) with the gathers served from LDS.
+ * Output rows are grouped into blocks (e.g. the cliques); each block lists its distinct source rows
+ * (<= 256), and scol gives, for every CSR entry, the slot of its source in its row's block.
+ *   blk_ptr  [n_blocks+1] int32 offsets into blk_rows; blk_rows: output rows (each exactly once)
+ *   src_ptr  [n_blocks+1] int32 offsets into src_rows; src_rows: input rows staged per block
+ *   row_ptr / val        the CSR of niidmix_mix_csr_f32 (int64 / fp32)
+ *   scol     [nnz] int32 slot (index into the block's source list) of every CSR entry
+ *   max_src  largest source list (selects the LDS footprint) */
+typedef struct niidmix_staged_plan {
+    int32_t n_blocks;
+    int32_t max_src;
+    const int32_t *blk_ptr;
+    const int32_t *blk_rows;
+    const int32_t *src_ptr;
+    const int32_t *src_rows;
+    const int64_t *row_ptr;
+    const int32_t *scol;
+    const float *val;
+} niidmix_staged_plan;
+
+int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                           const niidmix_staged_plan *plan, int mode, void *stream);
+
 /* Dense mixing Y = W^T X on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), for topologies dense
  * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).
  *   w  [n, n] fp32 row-major, w[src*n + dst] = W[src, dst] — the reference's topology['weights']

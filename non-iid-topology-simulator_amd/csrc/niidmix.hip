@@ -16,7 +16,7 @@
 // reference's separate ATen mul and add_ (model/__init__.py:24: c1.add_(w*p1)).
 //
 // Kernels:
-//   k_mix_csr<EXACT,VEC>   generic CSR gather, one wave per (output row, 256-column chunk);
+//   k_mix_csr<EXACT,VW>    generic CSR gather, one wave per (output row, 256-column chunk);
 //                          XCD-aware work order so the rows one chunk needs stay in that XCD's L2.
 //   k_mix_clique<RPW,G>    clique-factored: one 512-thread workgroup per (clique, 256-column chunk)
 //                          reads each member row ONCE from HBM into registers, forms the per-group
@@ -97,7 +97,23 @@ __device__ __forceinline__ float4 axpy4(float w, float4 xv, float4 acc) {
 // one output row.  Work order is XCD-aware: items t and t+8 share an XCD (round-robin dispatch),
 // and consecutive items on one XCD sweep all rows of the SAME chunk, so the chunk's source rows
 // (rows x 1 KiB) are reused from that XCD's L2 by every output row that gathers them.
-template <bool EXACT, bool VEC>
+// VW-wide loads/stores (VW = 4: float4, 2: float2, 1: float): a lane owns 4 columns of the chunk as
+// 4/VW slots, slot q covering columns c0 + VW*lane + 64*VW*q + [0, VW) (each wave-instruction reads
+// 64*VW contiguous floats).  VW is the widest width the slab's p, ld and alignment allow.
+template <int VW> __device__ __forceinline__ void ldv(const float *p, float *o);
+template <> __device__ __forceinline__ void ldv<4>(const float *p, float *o) {
+    const float4 v = *reinterpret_cast<const float4 *>(p); o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <> __device__ __forceinline__ void ldv<2>(const float *p, float *o) {
+    const float2 v = *reinterpret_cast<const float2 *>(p); o[0] = v.x; o[1] = v.y;
+}
+template <> __device__ __forceinline__ void ldv<1>(const float *p, float *o) { o[0] = *p; }
+template <int VW> __device__ __forceinline__ void stv_nt(float *p, const float *o) {
+#pragma unroll
+    for (int e = 0; e < VW; ++e) __builtin_nontemporal_store(o[e], p + e);
+}
+
+template <bool EXACT, int VW, int SPL>
 __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, int64_t ld_x,
                                                  float *__restrict__ y, int64_t ld_y,
                                                  int64_t n_rows, int64_t p,
@@ -106,6 +122,9 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
                                                  const float *__restrict__ val,
                                                  int64_t n_row_groups, int64_t n_items,
                                                  int avg_only) {
+    constexpr int S = 4 * SPL / VW;           // slots per lane
+    constexpr int NE = 4 * SPL;               // columns per lane
+    constexpr int64_t CH = kChunk * SPL;      // columns per (row, chunk) work item
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
     for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
@@ -113,55 +132,68 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
         const int64_t local = t >> 3;
         const int64_t chunk = (local / n_row_groups) * 8 + xcd;
         const int64_t row = (local % n_row_groups) * 4 + wave;
-        const int64_t c0 = chunk * kChunk;
+        const int64_t c0 = chunk * CH;
         if (row >= n_rows || c0 >= p) continue;  // wave-uniform
         const int64_t beg = row_ptr[row];
         const int64_t end = row_ptr[row + 1];
-        if constexpr (VEC) {
-            const int64_t c = c0 + 4 * lane;
-            if (c >= p) continue;
-            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (beg < end) {
-                const float4 xs = ld4(x + (int64_t)col[beg] * ld_x + c);
-                // self * 0: keeps -0.0 and turns inf/NaN into NaN, as p.mul_(0) does
-                z = make_float4(xs.x * 0.f, xs.y * 0.f, xs.z * 0.f, xs.w * 0.f);
-            }
-            float4 acc = z;
-            int64_t k = beg;
-            for (; k + 8 <= end; k += 8) {  // 8 independent loads in flight, then in-order accumulate
-                float4 xv[8];
+        int64_t cs[S];
+        bool ok[S];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) xv[u] = ld4(x + (int64_t)col[k + u] * ld_x + c);
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc = axpy4<EXACT>(val[k + u], xv[u], acc);
-            }
-            for (; k < end; ++k) acc = axpy4<EXACT>(val[k], ld4(x + (int64_t)col[k] * ld_x + c), acc);
-            // update_models: p.mul_(0.); p.add_(new)  ->  z + acc
-            const float4 out = avg_only ? acc : make_float4(z.x + acc.x, z.y + acc.y, z.z + acc.z, z.w + acc.w);
-            st4_nt(y + row * ld_y + c, out);
-        } else {
-            // scalar columns: lane handles c0 + lane + 64*q, q = 0..3 (coalesced per q)
-            float z[4], acc[4];
-            bool ok[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t c = c0 + lane + 64 * q;
-                ok[q] = c < p;
-                z[q] = 0.f;
-                if (ok[q] && beg < end) z[q] = x[(int64_t)col[beg] * ld_x + c] * 0.f;
-                acc[q] = z[q];
-            }
-            for (int64_t k = beg; k < end; ++k) {
-                const float w = val[k];
-                const float *src = x + (int64_t)col[k] * ld_x;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (ok[q]) acc[q] = axpy<EXACT>(w, src[c0 + lane + 64 * q], acc[q]);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (ok[q]) y[row * ld_y + c0 + lane + 64 * q] = avg_only ? acc[q] : z[q] + acc[q];
+        for (int q = 0; q < S; ++q) {
+            cs[q] = c0 + VW * lane + 64 * VW * q;
+            ok[q] = cs[q] < p;            // p % VW == 0: a slot is all-in or all-out
         }
+        float z[NE], acc[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) z[e] = 0.f;
+        if (beg < end) {
+            const float *xs = x + (int64_t)col[beg] * ld_x;
+#pragma unroll
+            for (int q = 0; q < S; ++q)
+                if (ok[q]) {
+                    ldv<VW>(xs + cs[q], z + q * VW);
+#pragma unroll
+                    for (int e = 0; e < VW; ++e)   // self * 0: keeps -0.0, inf/NaN -> NaN (p.mul_(0))
+                        z[q * VW + e] *= 0.f;
+                }
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[e] = z[e];
+        // U independent gathers in flight, then in-order accumulation (the exact mode's order)
+        constexpr int U = SPL >= 4 ? 4 : 8;
+        int64_t k = beg;
+        for (; k < end; k += U) {
+            float xv[U][NE];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool have = k + u < end;                 // wave-uniform
+                const float *src = x + (int64_t)col[have ? k + u : beg] * ld_x;
+#pragma unroll
+                for (int q = 0; q < S; ++q) {
+                    if (ok[q] && have) ldv<VW>(src + cs[q], xv[u] + q * VW);
+                    else {
+#pragma unroll
+                        for (int e = 0; e < VW; ++e) xv[u][q * VW + e] = 0.f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (k + u < end) {
+                    const float w = val[k + u];
+#pragma unroll
+                    for (int e = 0; e < NE; ++e) acc[e] = axpy<EXACT>(w, xv[u][e], acc[e]);
+                }
+            }
+        }
+        // update_models: p.mul_(0.); p.add_(new)  ->  z + acc   (AVERAGE_ONLY: acc)
+        float o[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+        float *dst = y + row * ld_y;
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+            if (ok[q]) stv_nt<VW>(dst + cs[q], o + q * VW);
     }
 }
 
@@ -364,19 +396,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 //   A[i][k] = W[k0+k][i0+i]  (LDS As[k][i]);  B[k][j] = X[k0+k][j0+j]  (LDS Bs[k][j])
 //   operand maps (32x32x2 f32): lane l holds A[l&31][l>>5], B[l>>5][l&31];
 //   C/D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15.
-constexpr int kDBM = 128, kDBN = 128, kDBK = 16, kDPad = 4;
+constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
-                                                   float *__restrict__ y, int64_t ld_y, int64_t n,
-                                                   int64_t p, const float *__restrict__ w,
-                                                   int64_t n_it, int64_t n_items) {
-    __shared__ float As[kDBK][kDBM + kDPad];
-    __shared__ float Bs[kDBK][kDBN + kDPad];
+// Software pipeline: the next K-step's A/B tiles are fetched into registers while the MFMAs of
+// the current step run; LDS is double-buffered so one barrier per K-step suffices.
+template <bool VEC, bool AVEC>
+__global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
+                                                      float *__restrict__ y, int64_t ld_y, int64_t n,
+                                                      int64_t p, const float *__restrict__ w,
+                                                      int64_t n_it, int64_t n_items) {
+    __shared__ float As[2][kDBK][kDBM + kDPad];
+    __shared__ float Bs[2][kDBK][kDBN + kDPad];
     const int tid = threadIdx.x;
     const int wave = wave_id();
     const int lane = tid & 63;
     const int wm = wave >> 1, wn = wave & 1;
+    // loader mapping: 32 rows x 128 cols = 4096 floats per operand, 16 per thread (4 x float4)
+    const int lk = tid >> 5;          // 0..7  (+8*h)
+    const int lc = (tid & 31) * 4;    // 0..124
     for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
         const int64_t xcd = t & 7;
         const int64_t local = t >> 3;
@@ -392,51 +429,59 @@ __global__ __launch_bounds__(256) void k_mix_dense(const float *__restrict__ x, 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-        // loader mapping: 16 rows x 128 cols = 2048 floats, 8 per thread as 2 x float4
-        const int lk = tid >> 4;          // 0..15
-        const int lc = (tid & 15) * 8;    // 0..120
-        for (int64_t k0 = 0; k0 < n; k0 += kDBK) {
-            float ra[8], rb[8];
-            const int64_t kr = k0 + lk;
+        float ra[4][4], rb[4][4];
+        auto fetch = [&](int64_t k0) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t i = i0 + lc + u;
-                ra[u] = (kr < n && i < n) ? w[kr * n + i] : 0.f;
-            }
-            if (VEC) {
+            for (int h = 0; h < 4; ++h) {
+                const int64_t kr = k0 + lk + 8 * h;
+                if (AVEC) {
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (kr < n && i0 + lc < n) v = ld4(w + kr * n + i0 + lc);
+                    ra[h][0] = v.x; ra[h][1] = v.y; ra[h][2] = v.z; ra[h][3] = v.w;
+                } else {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int64_t j = j0 + lc + 4 * h;
+                    for (int u = 0; u < 4; ++u) {
+                        const int64_t i = i0 + lc + u;
+                        ra[h][u] = (kr < n && i < n) ? w[kr * n + i] : 0.f;
+                    }
+                }
+                if (VEC) {
+                    const int64_t j = j0 + lc;
                     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (kr < n && j < p) v = ld4(x + kr * ld_x + j);
-                    rb[4 * h + 0] = v.x; rb[4 * h + 1] = v.y; rb[4 * h + 2] = v.z; rb[4 * h + 3] = v.w;
-                }
-            } else {
+                    rb[h][0] = v.x; rb[h][1] = v.y; rb[h][2] = v.z; rb[h][3] = v.w;
+                } else {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int64_t j = j0 + lc + u;
-                    rb[u] = (kr < n && j < p) ? x[kr * ld_x + j] : 0.f;
+                    for (int u = 0; u < 4; ++u) {
+                        const int64_t j = j0 + lc + u;
+                        rb[h][u] = (kr < n && j < p) ? x[kr * ld_x + j] : 0.f;
+                    }
                 }
             }
-            __syncthreads();
+        };
+        fetch(0);
+        int buf = 0;
+        for (int64_t k0 = 0; k0 < n; k0 += kDBK) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                As[lk][lc + u] = ra[u];
-                Bs[lk][lc + u] = rb[u];
+            for (int h = 0; h < 4; ++h) {
+                *reinterpret_cast<float4 *>(&As[buf][lk + 8 * h][lc]) = make_float4(ra[h][0], ra[h][1], ra[h][2], ra[h][3]);
+                *reinterpret_cast<float4 *>(&Bs[buf][lk + 8 * h][lc]) = make_float4(rb[h][0], rb[h][1], rb[h][2], rb[h][3]);
             }
             __syncthreads();
+            if (k0 + kDBK < n) fetch(k0 + kDBK);          // in flight during the MFMAs below
 #pragma unroll
             for (int kk = 0; kk < kDBK; kk += 2) {
                 const int kq = kk + (lane >> 5);
-                float a0 = As[kq][wm * 64 + (lane & 31)];
-                float a1 = As[kq][wm * 64 + 32 + (lane & 31)];
-                float b0 = Bs[kq][wn * 64 + (lane & 31)];
-                float b1 = Bs[kq][wn * 64 + 32 + (lane & 31)];
+                const float a0 = As[buf][kq][wm * 64 + (lane & 31)];
+                const float a1 = As[buf][kq][wm * 64 + 32 + (lane & 31)];
+                const float b0 = Bs[buf][kq][wn * 64 + (lane & 31)];
+                const float b1 = Bs[buf][kq][wn * 64 + 32 + (lane & 31)];
                 acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
                 acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
                 acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
             }
+            buf ^= 1;
         }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -446,9 +491,99 @@ __global__ __launch_bounds__(256) void k_mix_dense(const float *__restrict__ x, 
                 for (int r = 0; r < 16; ++r) {
                     const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                     const int64_t j = j0 + wn * 64 + b * 32 + (lane & 31);
-                    if (i < n && j < p) y[i * ld_y + j] = acc[a][b][r];
+                    if (i < n && j < p) __builtin_nontemporal_store(acc[a][b][r], y + i * ld_y + j);
                 }
+        __syncthreads();   // LDS buffers are rewritten by the next tile
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Block-staged CSR mixing (exact or fast).  Output rows are grouped into blocks (the cliques); a
+// block's distinct source rows (members + remote neighbours, <= 256) are staged ONCE per column
+// chunk in LDS, then every output row accumulates its CSR entries in the reference's order from
+// LDS.  HBM traffic ~ 2*4 B per node-parameter (+ remote rows), the gathers hit LDS instead of L2:
+// the exact mode's bound moves from L2 bandwidth (k_mix_csr) to LDS/VALU.
+// Chunk = 64 lanes x VPL floats.  Per-entry slot/weight are wave-uniform -> scalar loads.
+template <bool EXACT, int VPL>
+__global__ __launch_bounds__(256) void k_mix_staged(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_blocks, const int32_t *__restrict__ blk_ptr, const int32_t *__restrict__ blk_rows,
+    const int32_t *__restrict__ src_ptr, const int32_t *__restrict__ src_rows,
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ scol,
+    const float *__restrict__ val, int64_t n_items, int avg_only) {
+    extern __shared__ __attribute__((aligned(16))) float stage[];   // [n_src][64 * VPL]
+    constexpr int CW = 64 * VPL;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t chunk = (local / n_blocks) * 8 + xcd;
+        const int32_t b = (int32_t)(local % n_blocks);
+        const int64_t c0 = chunk * CW;
+        if (c0 >= p) continue;                              // block-uniform
+        const int64_t c = c0 + VPL * lane;
+        const bool act = c < p;                             // p % VPL == 0
+        const int32_t s0 = src_ptr[b], ns = src_ptr[b + 1] - s0;
+        // 1. stage the block's source rows (each wave a share of the rows, one row per instruction)
+        for (int32_t r = wave; r < ns; r += 4) {
+            const float *src = x + (int64_t)src_rows[s0 + r] * ld_x;
+            float v[VPL];
+#pragma unroll
+            for (int e = 0; e < VPL; ++e) v[e] = 0.f;
+            if (act) ldv<VPL>(src + c, v);
+#pragma unroll
+            for (int e = 0; e < VPL; ++e) stage[r * CW + VPL * lane + e] = v[e];
+        }
         __syncthreads();
+        // 2. every output row of the block, entries in CSR order, operands from LDS
+        const int32_t r0 = blk_ptr[b], nr = blk_ptr[b + 1] - r0;
+        for (int32_t i = wave; i < nr; i += 4) {
+            const int64_t row = blk_rows[r0 + i];
+            const int64_t beg = row_ptr[row], end = row_ptr[row + 1];
+            float z[VPL], acc[VPL];
+            {
+                const float *sp = stage + (int64_t)scol[beg] * CW + VPL * lane;
+#pragma unroll
+                for (int e = 0; e < VPL; ++e) { z[e] = sp[e] * 0.f; acc[e] = z[e]; }
+            }
+            // entry descriptors 64 at a time, lane-parallel (one vector load each), handed to the
+            // scalar unit by v_readlane: no scalar-load latency inside the accumulation chain
+            constexpr int U = 8;   // U LDS reads in flight, then in-order accumulation
+            for (int64_t kb = beg; kb < end; kb += 64) {
+                const int cnt = (int)(end - kb < 64 ? end - kb : 64);
+                const int d_s = lane < cnt ? scol[kb + lane] : 0;
+                const float d_w = lane < cnt ? val[kb + lane] : 0.f;
+                for (int j = 0; j < cnt; j += U) {
+                    float xv[U][VPL];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int slot = __builtin_amdgcn_readlane(d_s, j + u < cnt ? j + u : 0);
+                        const float *sp = stage + slot * CW + VPL * lane;
+                        if (VPL == 2) {
+                            const float2 t2 = *reinterpret_cast<const float2 *>(sp);
+                            xv[u][0] = t2.x; xv[u][VPL - 1] = t2.y;
+                        } else {
+                            xv[u][0] = sp[0];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (j + u < cnt) {
+                            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_w), j + u));
+#pragma unroll
+                            for (int e = 0; e < VPL; ++e) acc[e] = axpy<EXACT>(w, xv[u][e], acc[e]);
+                        }
+                }
+            }
+            if (act) {
+                float o[VPL];
+#pragma unroll
+                for (int e = 0; e < VPL; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+                stv_nt<VPL>(y + row * ld_y + c, o);
+            }
+        }
+        __syncthreads();                                    // stage[] is refilled by the next item
     }
 }
 
@@ -595,18 +730,25 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     if (x == y || (x > y && x < y + (n_rows - 1) * ld_y + p))
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const bool vec = (p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y);
-    const int64_t n_chunks = (p + kChunk - 1) / kChunk;
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    const int vw = (p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && (align & 15) == 0) ? 4
+                 : (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
+    // NIIDMIX_CSR_SPL=4: 4x wider work items (tuning; measured slower on ring-100, P=62006)
+    const char *spl_env = getenv("NIIDMIX_CSR_SPL");
+    const int spl = (spl_env && atoi(spl_env) == 4) ? 4 : 1;
+    const int64_t n_chunks = (p + kChunk * spl - 1) / (kChunk * spl);
     const int64_t n_row_groups = (n_rows + 3) / 4;
     const int64_t n_items = n_row_groups * ((n_chunks + 7) / 8) * 8;
     const dim3 grid((unsigned)grid_for(n_items)), block(256);
+#define NIIDMIX_CSR(E, V, S) hipLaunchKernelGGL((k_mix_csr<E, V, S>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only)
+#define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR(E, V, 4); else NIIDMIX_CSR(E, V, 1); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) {
-        if (vec) hipLaunchKernelGGL((k_mix_csr<true, true>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
-        else     hipLaunchKernelGGL((k_mix_csr<true, false>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+        if (vw == 4) NIIDMIX_CSR_S(true, 4); else if (vw == 2) NIIDMIX_CSR_S(true, 2); else NIIDMIX_CSR_S(true, 1);
     } else {
-        if (vec) hipLaunchKernelGGL((k_mix_csr<false, true>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
-        else     hipLaunchKernelGGL((k_mix_csr<false, false>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only);
+        if (vw == 4) NIIDMIX_CSR_S(false, 4); else if (vw == 2) NIIDMIX_CSR_S(false, 2); else NIIDMIX_CSR_S(false, 1);
     }
+#undef NIIDMIX_CSR_S
+#undef NIIDMIX_CSR
     return check_launch("k_mix_csr");
 }
 
@@ -631,6 +773,37 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, n_items, s);
 }
 
+int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                           const niidmix_staged_plan *plan, int mode, void *stream) {
+    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (p < 0 || plan->n_blocks < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (plan->n_blocks == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !plan->blk_ptr || !plan->blk_rows || !plan->src_ptr || !plan->src_rows ||
+        !plan->row_ptr || !plan->scol || !plan->val)
+        return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (plan->max_src < 1 || plan->max_src > 256)
+        return set_error(NIIDMIX_EUNSUPPORTED, "block with %d source rows (1..256 supported)", plan->max_src);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    const int vpl = (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0 && plan->max_src <= 160) ? 2 : 1;
+    const int64_t cw = 64 * vpl;
+    const int64_t n_chunks = (p + cw - 1) / cw;
+    const int64_t n_items = (int64_t)plan->n_blocks * ((n_chunks + 7) / 8) * 8;
+    const size_t lds = (size_t)plan->max_src * cw * sizeof(float);
+    const dim3 grid((unsigned)grid_for(n_items)), block(256);
+#define NIIDMIX_STAGED(E, V) hipLaunchKernelGGL((k_mix_staged<E, V>), grid, block, lds, s, x, ld_x, y, ld_y, p, plan->n_blocks, plan->blk_ptr, plan->blk_rows, plan->src_ptr, plan->src_rows, plan->row_ptr, plan->scol, plan->val, n_items, avg_only)
+    if (mode == NIIDMIX_MODE_EXACT) { if (vpl == 2) NIIDMIX_STAGED(true, 2); else NIIDMIX_STAGED(true, 1); }
+    else                            { if (vpl == 2) NIIDMIX_STAGED(false, 2); else NIIDMIX_STAGED(false, 1); }
+#undef NIIDMIX_STAGED
+    return check_launch("k_mix_staged");
+}
+
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
                           int64_t p, const float *w, void *stream) {
     if (n < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
@@ -645,8 +818,11 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     const int64_t n_jt = (p + kDBN - 1) / kDBN;
     const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
     const dim3 grid((unsigned)grid_for(n_items)), block(256);
-    if (vec) hipLaunchKernelGGL((k_mix_dense<true>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items);
-    else     hipLaunchKernelGGL((k_mix_dense<false>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items);
+    const bool avec = (n % 4 == 0) && aligned16(w);
+#define NIIDMIX_DENSE(V, A) hipLaunchKernelGGL((k_mix_dense<V, A>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items)
+    if (vec) { if (avec) NIIDMIX_DENSE(true, true); else NIIDMIX_DENSE(true, false); }
+    else     { if (avec) NIIDMIX_DENSE(false, true); else NIIDMIX_DENSE(false, false); }
+#undef NIIDMIX_DENSE
     return check_launch("k_mix_dense");
 }
 

@@ -29,6 +29,12 @@ class CliquePlanC(ctypes.Structure):
                 ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp)]
 
 
+class StagedPlanC(ctypes.Structure):
+    """Mirror of struct niidmix_staged_plan (include/niidmix.h)."""
+    _fields_ = [("n_blocks", _i32), ("max_src", _i32), ("blk_ptr", _vp), ("blk_rows", _vp),
+                ("src_ptr", _vp), ("src_rows", _vp), ("row_ptr", _vp), ("scol", _vp), ("val", _vp)]
+
+
 # every symbol include/niidmix.h declares, with its ctypes signature
 SIGNATURES = {
     "niidmix_abi_version": (ctypes.c_int, []),
@@ -37,6 +43,8 @@ SIGNATURES = {
                                            ctypes.c_int, _vp]),
     "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(CliquePlanC), _vp]),
+    "niidmix_mix_staged_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+                                              ctypes.POINTER(StagedPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_copy2d_async": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp]),

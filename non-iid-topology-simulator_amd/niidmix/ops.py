@@ -17,6 +17,7 @@ import torch
 
 from . import _lib
 from .factor import build_clique_plan
+from .staged import build_staged_plan
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -116,6 +117,31 @@ def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tens
     _lib.check(rc, "niidmix::mix_clique")
 
 
+@torch.library.custom_op("niidmix::mix_staged", mutates_args=("out",))
+def mix_staged(x: torch.Tensor, blk_ptr: torch.Tensor, blk_rows: torch.Tensor,
+               src_ptr: torch.Tensor, src_rows: torch.Tensor, row_ptr: torch.Tensor,
+               scol: torch.Tensor, val: torch.Tensor, out: torch.Tensor, max_src: int,
+               mode: int) -> None:
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    dev = x.device
+    nb = blk_ptr.numel() - 1
+    _vec("blk_ptr", blk_ptr, torch.int32, dev)
+    _vec("blk_rows", blk_rows, torch.int32, dev, out.shape[0])
+    _vec("src_ptr", src_ptr, torch.int32, dev, nb + 1)
+    _vec("src_rows", src_rows, torch.int32, dev)
+    _vec("row_ptr", row_ptr, torch.int64, dev, out.shape[0] + 1)
+    _vec("scol", scol, torch.int32, dev)
+    _vec("val", val, torch.float32, dev, scol.numel())
+    _no_overlap(x, out)
+    plan = _lib.StagedPlanC(nb, int(max_src), blk_ptr.data_ptr(), blk_rows.data_ptr(),
+                            src_ptr.data_ptr(), src_rows.data_ptr(), row_ptr.data_ptr(),
+                            scol.data_ptr(), val.data_ptr())
+    rc = _lib.lib.niidmix_mix_staged_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
+                                         ctypes.byref(plan), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_staged")
+
+
 @torch.library.custom_op("niidmix::mix_dense", mutates_args=("out",))
 def mix_dense(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
     _slab("x", x)
@@ -178,13 +204,22 @@ class Mixer:
             self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
             self.p_res_col = torch.from_numpy(p.res_col).to(dev)
             self.p_res_val = torch.from_numpy(p.res_val).to(dev)
+        self.staged, self.staged_reason = build_staged_plan(csr, cliques) if cliques else \
+            build_staged_plan(csr, None)
+        if self.staged is not None:
+            sp = self.staged
+            self.s_blk_ptr = torch.from_numpy(sp.blk_ptr).to(dev)
+            self.s_blk_rows = torch.from_numpy(sp.blk_rows).to(dev)
+            self.s_src_ptr = torch.from_numpy(sp.src_ptr).to(dev)
+            self.s_src_rows = torch.from_numpy(sp.src_rows).to(dev)
+            self.s_scol = torch.from_numpy(sp.scol).to(dev)
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
 
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
-            return "csr-exact"
+            return "staged-exact" if self.staged is not None else "csr-exact"
         if self.plan is not None and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:
@@ -199,6 +234,11 @@ class Mixer:
             mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT)
         elif k == "csr-fast":
             mix_csr(x, self.row_ptr, self.col, self.val, out, FAST)
+        elif k in ("staged-exact", "staged-fast"):
+            _req(self.staged is not None, f"no staged plan: {self.staged_reason}")
+            mix_staged(x, self.s_blk_ptr, self.s_blk_rows, self.s_src_ptr, self.s_src_rows,
+                       self.row_ptr, self.s_scol, self.val, out, self.staged.max_src,
+                       EXACT if k == "staged-exact" else FAST)
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,

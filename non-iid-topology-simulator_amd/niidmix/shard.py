@@ -120,6 +120,56 @@ class ShardPlan:
         return LocalShard(r, nodes, halo, halo_owner, lcsr, cliques, send)
 
 
+class DistTransport:
+    """Halo exchange over torch.distributed point-to-point (RCCL on GPUs, gloo on CPU): per window,
+    one grouped batch_isend_irecv with every peer."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def exchange(self, sm, k, xk):
+        ops = []
+        for q in sorted(set(sm.send_idx) | set(sm.recv)):
+            if q in sm.send_idx:
+                sb = sm.send_buf[q][k]
+                torch.index_select(xk[:sm.n_local], 0, sm.send_idx[q], out=sb)
+                ops.append(dist.P2POp(dist.isend, sb, q, group=self.group))
+            if q in sm.recv:
+                r0, cnt = sm.recv[q]
+                ops.append(dist.P2POp(dist.irecv, xk[r0:r0 + cnt], q, group=self.group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    @staticmethod
+    def wait(handle):
+        for wk in handle:
+            wk.wait()                          # NCCL: the current stream waits, not the host
+
+
+class LoopbackTransport:
+    """Single-process stand-in for the RCCL exchange (tests on one GPU): every rank's ShardedMixer
+    lives in this process; before a round the caller sets `inputs[rank]` to each rank's input slab
+    and the exchange copies the rows a rank needs straight out of its peers' slabs."""
+
+    def __init__(self):
+        self.peers = {}
+        self.inputs = {}
+
+    def exchange(self, sm, k, xk):
+        for q, (r0, cnt) in sorted(sm.recv.items()):
+            peer = self.peers[q]
+            src = self.inputs[q][k][:peer.n_local]
+            xk[r0:r0 + cnt].copy_(src.index_select(0, peer.send_idx[sm.rank]))
+        ev = torch.cuda.Event() if xk.is_cuda else None
+        if ev is not None:
+            ev.record(torch.cuda.current_stream(xk.device))
+        return ev
+
+    @staticmethod
+    def wait(handle):
+        if handle is not None:
+            torch.cuda.current_stream().wait_event(handle)
+
+
 def window_layout(p, windows):
     """(K, w): K column windows of w columns (w multiple of 256 so every window stays aligned)."""
     k = max(1, min(windows, (p + 255) // 256))
@@ -134,7 +184,8 @@ class ShardedMixer:
     x, out: window-blocked slabs [K, rows_in, w] (see empty()); columns >= p of the last window are
     padding.  compute(x2d, out2d, kernel) defaults to this rank's Mixer on its GPU."""
 
-    def __init__(self, csr, cliques, world, rank, device, p, windows=8, group=None, compute=None):
+    def __init__(self, csr, cliques, world, rank, device, p, windows=8, group=None, compute=None,
+                 transport=None):
         self.plan = ShardPlan(csr, cliques, world)
         self.shard = self.plan.local(rank)
         self.world, self.rank, self.group = world, rank, group
@@ -159,7 +210,10 @@ class ShardedMixer:
         self.halo_rows = len(self.shard.halo)
         self.is_cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.is_cuda else None
-        if world > 1:
+        self.transport = transport if transport is not None else DistTransport(group)
+        if isinstance(self.transport, LoopbackTransport):
+            self.transport.peers[rank] = self
+        elif world > 1:
             dist.barrier(group=group)   # first collective: every rank joins before any P2P
 
     @classmethod
@@ -181,18 +235,6 @@ class ShardedMixer:
     def _gpu_compute(self, x2d, out2d, kernel=None, mode="fast"):
         self.mixer(x2d, out=out2d, kernel=kernel, mode=mode)
 
-    def _exchange(self, xk, slot):
-        ops = []
-        for q in sorted(set(self.send_idx) | set(self.recv)):
-            if q in self.send_idx:
-                sb = self.send_buf[q][slot]
-                torch.index_select(xk[:self.n_local], 0, self.send_idx[q], out=sb)
-                ops.append(dist.P2POp(dist.isend, sb, q, group=self.group))
-            if q in self.recv:
-                r0, cnt = self.recv[q]
-                ops.append(dist.P2POp(dist.irecv, xk[r0:r0 + cnt], q, group=self.group))
-        return dist.batch_isend_irecv(ops) if ops else []
-
     def __call__(self, x, out, kernel=None, mode="fast", events=None):
         assert x.shape == (self.k, self.rows_in, self.w) and out.shape == x.shape
         cur = torch.cuda.current_stream(self.device) if self.is_cuda else None
@@ -205,14 +247,14 @@ class ShardedMixer:
             if self.world > 1:
                 if self.is_cuda:
                     with torch.cuda.stream(self.comm_stream):
-                        pending.append(self._exchange(x[k], k))
+                        pending.append(self.transport.exchange(self, k, x[k]))
                 else:
-                    pending.append(self._exchange(x[k], k))
+                    pending.append(self.transport.exchange(self, k, x[k]))
             else:
-                pending.append([])
+                pending.append(None)
         for k in range(self.k):
-            for wk in pending[k]:
-                wk.wait()                          # NCCL: the current stream waits, not the host
+            if pending[k] is not None:
+                self.transport.wait(pending[k])
             cw = min(self.w, self.p - k * self.w)
             self.compute(x[k][:, :cw], out[k][:self.n_local, :cw], kernel=kernel, mode=mode)
         if events is not None:

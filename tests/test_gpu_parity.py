@@ -27,16 +27,19 @@ def _mixer(g, dev, **kw):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-def test_exact_kernel_bitwise_vs_golden(name, gpu, oracle_mod):
+@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact"])
+def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     m = _mixer(g, gpu)
+    if kernel == "staged-exact" and m.staged is None:
+        pytest.skip(f"no staged plan: {m.staged_reason}")
     x = torch.from_numpy(g["x"]).to(gpu)
-    y = m(x, mode="exact").cpu().numpy()
+    y = m(x, kernel=kernel).cpu().numpy()
     assert oracle_mod.bitwise_equal(y, g["y"]), name
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense"])
+@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "staged-fast"])
 def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     if not np.all(np.isfinite(g["x"])):
@@ -45,6 +48,8 @@ def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
     p = g["x"].shape[1]
     if kernel == "clique" and (m.plan is None or p % 4):
         pytest.skip(f"no clique plan ({m.plan_reason}) or p % 4")
+    if kernel == "staged-fast" and m.staged is None:
+        pytest.skip(f"no staged plan ({m.staged_reason})")
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel=kernel).cpu().numpy()
     bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
@@ -56,7 +61,7 @@ def test_auto_kernel_choice(gpu):
     g = load_golden("dcliques1000_fc_p64")
     m = _mixer(g, gpu)
     assert m.kernel_for("fast") == "clique"
-    assert m.kernel_for("exact") == "csr-exact"
+    assert m.kernel_for("exact") == "staged-exact"
     g = load_golden("fc64_p33")
     assert _mixer(g, gpu).kernel_for("fast") == "dense"
     g = load_golden("ring100_p257")
@@ -75,12 +80,13 @@ def _windows(p, w=2048):
     return [(0, w), (p // 2 - w // 2, p // 2 + w // 2), (p - w, p)]
 
 
-def test_full_size_exact_windows(gpu, oracle_mod):
-    """BASELINE configs[2] at full size (N=1000 d-cliques, P=2^20): exact kernel is bit-identical
+@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact"])
+def test_full_size_exact_windows(kernel, gpu, oracle_mod):
+    """BASELINE configs[2] at full size (N=1000 d-cliques, P=2^20): exact kernels are bit-identical
     to the oracle on sampled column windows (columns are independent)."""
     p = 1 << 20
     g, m, x = _dcliques_full(gpu, p)
-    y = m(x, mode="exact")
+    y = m(x, kernel=kernel)
     for c0, c1 in _windows(p):
         xw = x[:, c0:c1].cpu().numpy()
         ref = oracle_mod.mix_exact_c(xw, g["row_ptr"], g["col"], g["val"])
