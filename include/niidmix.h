@@ -88,9 +88,10 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *   coef         [n_members * (1 + n_groups)] fp32: a_m, then c_{m,0..n_groups-1}
  *   res_ptr      [n_members+1] int32 offsets into res_col/res_val (residual sparse terms)
  *   res_col      [n_res] int32 input rows, res_val [n_res] fp32
- *   max_clique   largest clique size (selects the register tile; <= 256 supported)
- *   max_clique_res  largest number of residual terms of one clique (res_ptr[end]-res_ptr[begin]
- *                over its members); <= 64 supported (<= 16 when max_clique > 128)
+ *   max_clique   largest clique size: <= 256 selects a register tile (one HBM read per
+ *                parameter); larger cliques (e.g. fully-connected = one clique) use a two-pass
+ *                kernel whose second read is served from L2 / Infinity Cache
+ *   max_clique_res  largest number of residual terms of one clique (informational, >= 0)
  *   n_groups     1..4 */
 typedef struct niidmix_clique_plan {
     int32_t n_cliques;

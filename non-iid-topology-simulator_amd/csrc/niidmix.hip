@@ -498,6 +498,84 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
 }
 
 // ----------------------------------------------------------------------------------------------
+// Clique-factored mixing for BIG cliques (> 256 members, e.g. a fully-connected topology with MH
+// weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), 4 waves, lane = one
+// column.  Pass 1 streams the members (wave w: a contiguous quarter) into per-group sums, an LDS
+// reduction combines the waves; pass 2 streams the members again and writes
+// y = a x + sum_g c_g S_g (+ residual terms).  The pass-2 re-read (M x 256 B per item) is served
+// from L2 / the 256 MiB Infinity Cache, so HBM sees ~1 read + 1 write per parameter: an
+// HBM-bound alternative to the MFMA GEMM for dense-but-structured W.
+template <int G>
+__global__ __launch_bounds__(256) void k_mix_bigclique(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
+    const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
+    const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
+    constexpr int U = 8;
+    __shared__ float red[G][4][kWave];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t chunk = (local / n_cliques) * 8 + xcd;
+        const int32_t cq = (int32_t)(local % n_cliques);
+        const int64_t c0 = chunk * kWave;
+        if (c0 >= p) continue;                               // block-uniform
+        const bool act = c0 + lane < p;
+        const unsigned lo = act ? (unsigned)lane : 0u;
+        const float *xc = x + c0;
+        float *yc = y + c0;
+        const int32_t m0 = clique_ptr[cq];
+        const int32_t M = clique_ptr[cq + 1] - m0;
+        const int32_t per = (M + 3) / 4;
+        const int32_t kb = m0 + wave * per;
+        const int32_t ke = m0 + ((wave + 1) * per < M ? (wave + 1) * per : M);
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+        for (int32_t k = kb; k < ke; k += U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = xc[(int64_t)member_row[k + u < ke ? k + u : kb] * ld_x + lo];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k + u < ke) {
+                    const int gr = member_group[k + u];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) s[g] += gr == g ? v[u] : 0.f;
+                }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = (red[g][0][lane] + red[g][1][lane]) + (red[g][2][lane] + red[g][3][lane]);
+        __syncthreads();                                      // red[] is rewritten by the next item
+        for (int32_t k = kb; k < ke; k += U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = xc[(int64_t)member_row[k + u < ke ? k + u : kb] * ld_x + lo];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k + u < ke) {
+                    const int32_t m = k + u;
+                    const float *cf = coef + (int64_t)m * (1 + G);
+                    float o = cf[0] * v[u];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g], o);
+                    for (int32_t q = res_ptr[m]; q < res_ptr[m + 1]; ++q)
+                        o = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x + lo], o);
+                    if (act) __builtin_nontemporal_store(o, yc + (int64_t)member_row[m] * ld_y + lane);
+                }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Block-staged CSR mixing (exact or fast).  Output rows are grouped into blocks (the cliques); a
 // block's distinct source rows (members + remote neighbours, <= 256) are staged ONCE per column
 // chunk in LDS, then every output row accumulates its CSR entries in the reference's order from
@@ -762,10 +840,23 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
     if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
-    if (plan->max_clique > 256)
-        return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", plan->max_clique);
     if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (plan->max_clique > 256) {                     // big cliques: two-pass, one lane per column
+        const int64_t n_ch = (p + kWave - 1) / kWave;
+        const int64_t items = (int64_t)plan->n_cliques * ((n_ch + 7) / 8) * 8;
+        const dim3 grid((unsigned)grid_for(items)), block(256);
+#define NIIDMIX_BIG(G) hipLaunchKernelGGL((k_mix_bigclique<G>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, items)
+        switch (plan->n_groups) {
+            case 1: NIIDMIX_BIG(1); break;
+            case 2: NIIDMIX_BIG(2); break;
+            case 3: NIIDMIX_BIG(3); break;
+            case 4: NIIDMIX_BIG(4); break;
+            default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+        }
+#undef NIIDMIX_BIG
+        return check_launch("k_mix_bigclique");
+    }
     const int64_t n_chunks = (p + kChunk - 1) / kChunk;
     const int64_t n_items = (int64_t)plan->n_cliques * ((n_chunks + 7) / 8) * 8;
     if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))

@@ -23,8 +23,7 @@ from dataclasses import dataclass
 import numpy as np
 
 MAX_GROUPS = 4          # template limit of k_mix_clique
-MAX_CLIQUE = 256        # register rows of k_mix_clique_wave (one lane per column)
-MAX_CLIQUE_RES = 64     # residual source rows prefetched per clique (16 when a clique > 128)
+MAX_CLIQUE = 1 << 20    # <= 256: register-tiled k_mix_clique; larger: two-pass k_mix_bigclique
 
 
 @dataclass
@@ -184,9 +183,6 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
         return None, f"{n_res} residual terms > {max_res_per_node} per node"
     per_clique = res_ptr[clique_ptr[1:]] - res_ptr[clique_ptr[:-1]]
     max_cr = int(per_clique.max()) if len(per_clique) else 0
-    cap = MAX_CLIQUE_RES if biggest <= 128 else 16
-    if max_cr > cap:
-        return None, f"a clique has {max_cr} residual terms > {cap}"
     plan = CliquePlan(n=n, n_groups=G, max_clique=biggest, max_clique_res=max_cr,
                       clique_ptr=clique_ptr,
                       member_row=member_row, member_group=member_group, coef=coef,

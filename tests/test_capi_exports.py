@@ -50,6 +50,11 @@ def test_argument_errors_without_gpu():
     plan = _lib.CliquePlanC(1, 4, 5, 4, 0, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
     assert rc == _lib.EUNSUPPORTED   # n_groups 5
-    plan = _lib.CliquePlanC(1, 300, 2, 300, 0, 8, 8, 8, 8, 8, 8, 8)
+    plan = _lib.CliquePlanC(1, 300, 2, 300, -1, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
-    assert rc == _lib.EUNSUPPORTED   # clique > 256
+    assert rc == _lib.EINVAL         # negative max_clique_res
+    sp = _lib.StagedPlanC(1, 300, 8, 8, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_staged_f32(16, 4, 1024, 4, 4, ctypes.byref(sp), 0, None)
+    assert rc == _lib.EUNSUPPORTED   # more than 256 staged source rows
+    rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
+    assert rc == _lib.EINVAL

@@ -61,9 +61,19 @@ def test_auto_kernel_choice(gpu):
     g = load_golden("dcliques1000_fc_p64")
     m = _mixer(g, gpu)
     assert m.kernel_for("fast") == "clique"
-    assert m.kernel_for("exact") == "staged-exact"
+    assert m.kernel_for("exact") == "csr-exact"
     g = load_golden("fc64_p33")
-    assert _mixer(g, gpu).kernel_for("fast") == "dense"
+    assert _mixer(g, gpu).kernel_for("fast") == "clique"      # MH fully-connected = one clique
+    ops = _ops()
+    rng = np.random.default_rng(0)
+    n = 128
+    w = rng.random((n, n)).astype(np.float32)
+    w /= w.sum(0, keepdims=True)                               # dense, column-stochastic, no structure
+    csr = ops.csr_from_numpy(np.arange(0, n * n + 1, n),
+                             np.concatenate([[i] + [j for j in range(n) if j != i] for i in range(n)]),
+                             np.concatenate([[w[i, i]] + [w[j, i] for j in range(n) if j != i]
+                                             for i in range(n)]))
+    assert ops.Mixer(csr=csr, device=gpu).kernel_for("fast") == "dense"
     g = load_golden("ring100_p257")
     assert _mixer(g, gpu).kernel_for("fast") == "csr-fast"
 
@@ -172,18 +182,19 @@ def test_mean_rows_and_distance(gpu, oracle_mod):
     assert oracle_mod.bitwise_equal(mean[:4096].cpu().numpy(), ref)
 
 
-def test_dense_mfma_fc1000(gpu, oracle_mod):
-    """configs[3] shape (fully-connected N=1000, MH weights) at reduced P: MFMA kernel within the
-    tolerance of the oracle."""
+@pytest.mark.parametrize("kernel", ["dense", "clique"])
+def test_fc1000_dense_and_factored(kernel, gpu, oracle_mod):
+    """configs[3] shape (fully-connected N=1000, MH weights) at reduced P: the MFMA GEMM and the
+    big-clique factored kernel (two-pass) both within the tolerance of the oracle."""
     from niidmix.topology import mh_csr
     n = 1000
     edges = {i: [j for j in range(n) if j != i] for i in range(n)}
     csr = mh_csr(n, edges)
     ops = _ops()
     m = ops.Mixer(csr=csr, device=gpu)
-    assert m.kernel_for("fast") == "dense"
+    assert m.plan is not None and m.plan.max_clique == 1000
     x = torch.randn(n, 4096 + 12, device=gpu)
-    y = m(x, kernel="dense").cpu().numpy()
+    y = m(x, kernel=kernel).cpu().numpy()
     xn = x.cpu().numpy()
     ref = oracle_mod.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
     bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
