@@ -27,14 +27,17 @@ from .topology import MixCSR
 
 
 class LocalShard:
-    def __init__(self, rank, nodes, halo, halo_owner, csr, cliques, send):
+    def __init__(self, rank, nodes, halo, halo_owner, csr, cliques, send_block, send_shared,
+                 recv):
         self.rank = rank
-        self.nodes = nodes            # global ids of local rows, local order
-        self.halo = halo              # global ids of halo rows (grouped by owner)
-        self.halo_owner = halo_owner  # owner rank of each halo row
-        self.csr = csr                # MixCSR over local rows, n_in = n_local + n_halo
-        self.cliques = cliques        # local cliques (local indices) or None
-        self.send = send              # {peer: local indices peer needs, in peer's halo order}
+        self.nodes = nodes              # global ids of local rows, local order
+        self.halo = halo                # global ids of halo rows (grouped by owner)
+        self.halo_owner = halo_owner    # owner rank of each halo row
+        self.csr = csr                  # MixCSR over local rows, n_in = n_local + n_halo
+        self.cliques = cliques          # local cliques (local indices) or None
+        self.send_block = send_block    # {peer: (a, b)}: local rows [a, b) only that peer reads
+        self.send_shared = send_shared  # {peer: local indices of rows several peers read}
+        self.recv = recv                # {peer: (first halo row, n_block, n_shared)}
 
     @property
     def n_local(self):
@@ -44,22 +47,27 @@ class LocalShard:
     def rows_in(self):
         return len(self.nodes) + len(self.halo)
 
-    def recv_ranges(self):
-        """{peer: (first halo row, count)} — contiguous per owner."""
+    @property
+    def send(self):
+        """{peer: every local index that peer reads, in the peer's halo order}."""
         out = {}
-        for q in np.unique(self.halo_owner):
-            idx = np.nonzero(self.halo_owner == q)[0]
-            out[int(q)] = (self.n_local + int(idx[0]), len(idx))
+        for q in sorted(set(self.send_block) | set(self.send_shared)):
+            a, b = self.send_block.get(q, (0, 0))
+            out[q] = np.concatenate([np.arange(a, b), self.send_shared.get(q, np.zeros(0, np.int64))])
         return out
 
 
 class ShardPlan:
+    """Clique-aligned partition + halo plan, computed identically on every rank.
+
+    Local row order of rank r: for each peer q (ascending) the rows ONLY q reads (a contiguous block:
+    sent zero-copy, straight out of the slab), then rows several peers read (packed per peer), then
+    interior rows.  The kernels address rows through the CSR / clique plan, so any order works;
+    each row's operand order is unchanged (bit-exact)."""
+
     def __init__(self, csr, cliques, world):
         n = csr.n
-        if cliques:
-            groups = [list(c) for c in cliques]
-        else:
-            groups = [[i] for i in range(n)]
+        groups = [list(c) for c in cliques] if cliques else [[i] for i in range(n)]
         sizes = np.asarray([len(c) for c in groups])
         # contiguous runs of groups, balanced by node count
         cuts = np.searchsorted(np.cumsum(sizes), np.arange(1, world) * n / world, side="left")
@@ -67,32 +75,77 @@ class ShardPlan:
         cuts = np.maximum.accumulate(cuts)
         self.world = world
         self.csr = csr
+        self.has_cliques = bool(cliques)
         self.groups_of = [groups[cuts[r]:cuts[r + 1]] for r in range(world)]
         self.owner = np.empty(n, np.int64)
-        self.local_index = np.empty(n, np.int64)
-        self.nodes_of = []
         for r in range(world):
-            nodes = [v for c in self.groups_of[r] for v in c]
-            self.nodes_of.append(np.asarray(nodes, np.int64))
-            self.owner[nodes] = r
-            self.local_index[nodes] = np.arange(len(nodes))
-        self.has_cliques = bool(cliques)
-        self._halo = [self._halo_of(r) for r in range(world)]
+            for c in self.groups_of[r]:
+                self.owner[c] = r
+        rp, col = csr.row_ptr, csr.col
+        # need[q]: remote rows rank q reads; readers[v]: ranks that read row v remotely
+        self.need = [set() for _ in range(world)]
+        dst_owner = np.repeat(self.owner, np.diff(rp))
+        remote = self.owner[col] != dst_owner
+        for q, v in zip(dst_owner[remote].tolist(), col[remote].tolist()):
+            self.need[q].add(v)
+        readers = {}
+        for q in range(world):
+            for v in self.need[q]:
+                readers.setdefault(v, []).append(q)
+        self.readers = readers
+        self.local_index = np.empty(n, np.int64)
+        self.nodes_of, self.blocks_of, self.shared_of = [], [], []
+        for r in range(world):
+            members = [v for c in self.groups_of[r] for v in c]
+            excl = {q: [] for q in range(world)}
+            shared, interior = [], []
+            for v in members:
+                rd = readers.get(v)
+                if not rd:
+                    interior.append(v)
+                elif len(rd) == 1:
+                    excl[rd[0]].append(v)
+                else:
+                    shared.append(v)
+            order, blocks = [], {}
+            for q in range(world):
+                e = sorted(excl[q])
+                if e:
+                    blocks[q] = (len(order), len(order) + len(e))
+                    order.extend(e)
+            shared.sort()
+            order.extend(shared)
+            order.extend(interior)
+            order = np.asarray(order, np.int64)
+            self.local_index[order] = np.arange(len(order))
+            self.nodes_of.append(order)
+            self.blocks_of.append(blocks)
+            self.shared_of.append(shared)
 
     def _halo_of(self, r):
-        rp, col = self.csr.row_ptr, self.csr.col
-        nodes = self.nodes_of[r]
-        need = set()
-        for g in nodes:
-            need.update(int(c) for c in col[rp[g]:rp[g + 1]] if self.owner[c] != r)
-        halo = sorted(need, key=lambda v: (self.owner[v], v))
-        return np.asarray(halo, np.int64)
+        """Rows rank r reads remotely, grouped by owner: per owner q, q's block for r then the
+        shared rows of q that r reads (both in q's local order)."""
+        halo, owners, recv = [], [], {}
+        start = 0
+        for q in range(self.world):
+            if q == r:
+                continue
+            a, b = self.blocks_of[q].get(r, (0, 0))
+            blk = self.nodes_of[q][a:b].tolist()
+            sh = [v for v in self.shared_of[q] if v in self.need[r]]
+            sh.sort(key=lambda v: self.local_index[v])
+            if blk or sh:
+                recv[q] = (start, len(blk), len(sh))
+                halo.extend(blk + sh)
+                owners.extend([q] * (len(blk) + len(sh)))
+                start += len(blk) + len(sh)
+        return np.asarray(halo, np.int64), np.asarray(owners, np.int64), recv
 
     def local(self, r):
         nodes = self.nodes_of[r]
-        halo = self._halo[r]
-        halo_owner = self.owner[halo] if len(halo) else np.zeros(0, np.int64)
+        halo, halo_owner, recv0 = self._halo_of(r)
         nl = len(nodes)
+        recv = {q: (nl + s0, nb, ns) for q, (s0, nb, ns) in recv0.items()}
         remap = {int(g): nl + i for i, g in enumerate(halo)}
         rp, col, val = self.csr.row_ptr, self.csr.col, self.csr.val
         counts, cols, vals = [], [], []
@@ -109,34 +162,46 @@ class ShardPlan:
         cliques = None
         if self.has_cliques:
             cliques = [[int(self.local_index[v]) for v in c] for c in self.groups_of[r]]
-        send = {}
+        send_shared = {}
         for q in range(self.world):
             if q == r:
                 continue
-            h = self._halo[q]
-            mine = h[self.owner[h] == r] if len(h) else h
-            if len(mine):
-                send[q] = self.local_index[mine]
-        return LocalShard(r, nodes, halo, halo_owner, lcsr, cliques, send)
+            sh = [v for v in self.shared_of[r] if v in self.need[q]]
+            if sh:
+                send_shared[q] = np.asarray(sorted(self.local_index[v] for v in sh), np.int64)
+        return LocalShard(r, nodes, halo, halo_owner, lcsr, cliques, dict(self.blocks_of[r]),
+                          send_shared, recv)
+
+    @property
+    def _halo(self):
+        return [self._halo_of(r)[0] for r in range(self.world)]
 
 
 class DistTransport:
     """Halo exchange over torch.distributed point-to-point (RCCL on GPUs, gloo on CPU): per window,
-    one grouped batch_isend_irecv with every peer."""
+    one grouped batch_isend_irecv with every peer.  A peer's exclusive rows go straight out of the
+    slab (one contiguous block, no copy); rows several peers read are packed (index_select)."""
 
     def __init__(self, group=None):
         self.group = group
 
     def exchange(self, sm, k, xk):
         ops = []
-        for q in sorted(set(sm.send_idx) | set(sm.recv)):
-            if q in sm.send_idx:
+        sh = sm.shard
+        for q in sorted(set(sh.send_block) | set(sh.send_shared) | set(sh.recv)):
+            a, b = sh.send_block.get(q, (0, 0))
+            if b > a:
+                ops.append(dist.P2POp(dist.isend, xk[a:b], q, group=self.group))
+            if q in sm.shared_idx:
                 sb = sm.send_buf[q][k]
-                torch.index_select(xk[:sm.n_local], 0, sm.send_idx[q], out=sb)
+                torch.index_select(xk[:sm.n_local], 0, sm.shared_idx[q], out=sb)
                 ops.append(dist.P2POp(dist.isend, sb, q, group=self.group))
-            if q in sm.recv:
-                r0, cnt = sm.recv[q]
-                ops.append(dist.P2POp(dist.irecv, xk[r0:r0 + cnt], q, group=self.group))
+            if q in sh.recv:
+                r0, nb, ns = sh.recv[q]
+                if nb:
+                    ops.append(dist.P2POp(dist.irecv, xk[r0:r0 + nb], q, group=self.group))
+                if ns:
+                    ops.append(dist.P2POp(dist.irecv, xk[r0 + nb:r0 + nb + ns], q, group=self.group))
         return dist.batch_isend_irecv(ops) if ops else []
 
     @staticmethod
@@ -155,10 +220,11 @@ class LoopbackTransport:
         self.inputs = {}
 
     def exchange(self, sm, k, xk):
-        for q, (r0, cnt) in sorted(sm.recv.items()):
+        for q, (r0, nb, ns) in sorted(sm.shard.recv.items()):
             peer = self.peers[q]
             src = self.inputs[q][k][:peer.n_local]
-            xk[r0:r0 + cnt].copy_(src.index_select(0, peer.send_idx[sm.rank]))
+            idx = torch.from_numpy(peer.shard.send[sm.rank]).to(xk.device)
+            xk[r0:r0 + nb + ns].copy_(src.index_select(0, idx))
         ev = torch.cuda.Event() if xk.is_cuda else None
         if ev is not None:
             ev.record(torch.cuda.current_stream(xk.device))
@@ -200,13 +266,12 @@ class ShardedMixer:
             self.mixer = Mixer(csr=self.shard.csr, cliques=self.shard.cliques, device=self.device)
             compute = self._gpu_compute
         self.compute = compute
-        self.recv = self.shard.recv_ranges()
-        self.send_idx = {q: torch.from_numpy(np.asarray(v, np.int64)).to(self.device)
-                         for q, v in self.shard.send.items()}
-        # one send buffer per (peer, window): a window's buffer is rewritten only in the next round,
+        self.shared_idx = {q: torch.from_numpy(np.asarray(v, np.int64)).to(self.device)
+                           for q, v in self.shard.send_shared.items()}
+        # one pack buffer per (peer, window): a window's buffer is rewritten only in the next round,
         # after this round's compute of that window has waited for its transfer
         self.send_buf = {q: [torch.empty((len(v), self.w), dtype=torch.float32, device=self.device)
-                             for _ in range(self.k)] for q, v in self.shard.send.items()}
+                             for _ in range(self.k)] for q, v in self.shard.send_shared.items()}
         self.halo_rows = len(self.shard.halo)
         self.is_cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.is_cuda else None
