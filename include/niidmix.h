@@ -56,6 +56,10 @@ enum niidmix_mode {
  * only in the sign of an exactly-zero result. */
 #define NIIDMIX_FLAG_AVERAGE_ONLY 2
 
+/* OR-ed into `mode` of niidmix_mix_csr_f32: performance hint, the graph's average row length
+ * (in-degree + 1) is <= 4 (ring, grid): fewer speculative gathers per batch.  Results unchanged. */
+#define NIIDMIX_FLAG_LOW_DEGREE 4
+
 /* ABI version (NIIDMIX_ABI_VERSION). */
 int niidmix_abi_version(void);
 
@@ -72,6 +76,7 @@ const char *niidmix_last_error(void);
  *            (the reference's models[0] = self, d_sgd.py:105)
  *   val      [nnz] fp32 weights (device): val = W[src, rank] (d_sgd.py:106), self weight first
  *   mode     NIIDMIX_MODE_EXACT or NIIDMIX_MODE_FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY
+ *            | NIIDMIX_FLAG_LOW_DEGREE
  * Rows with no entries are written as +0. */
 int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                         int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,

@@ -113,7 +113,7 @@ template <int VW> __device__ __forceinline__ void stv_nt(float *p, const float *
     for (int e = 0; e < VW; ++e) __builtin_nontemporal_store(o[e], p + e);
 }
 
-template <bool EXACT, int VW, int SPL>
+template <bool EXACT, int VW, int SPL, int U>
 __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, int64_t ld_x,
                                                  float *__restrict__ y, int64_t ld_y,
                                                  int64_t n_rows, int64_t p,
@@ -136,54 +136,47 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
         if (row >= n_rows || c0 >= p) continue;  // wave-uniform
         const int64_t beg = row_ptr[row];
         const int64_t end = row_ptr[row + 1];
+        // Column of each slot; slots past p read column c0 instead (loads stay unconditional — a
+        // branch around a load makes hipcc drain vmcnt per load) and are never stored.
         int64_t cs[S];
         bool ok[S];
 #pragma unroll
         for (int q = 0; q < S; ++q) {
-            cs[q] = c0 + VW * lane + 64 * VW * q;
-            ok[q] = cs[q] < p;            // p % VW == 0: a slot is all-in or all-out
+            const int64_t cq = c0 + VW * lane + 64 * VW * q;
+            ok[q] = cq < p;                   // p % VW == 0: a slot is all-in or all-out
+            cs[q] = ok[q] ? cq : c0;
         }
         float z[NE], acc[NE];
 #pragma unroll
-        for (int e = 0; e < NE; ++e) z[e] = 0.f;
-        if (beg < end) {
-            const float *xs = x + (int64_t)col[beg] * ld_x;
+        for (int e = 0; e < NE; ++e) { z[e] = 0.f; acc[e] = 0.f; }
+        for (int64_t kb = beg; kb < end; kb += 64) {
+            // 64 entries' (source row, weight) fetched lane-parallel, handed out by v_readlane:
+            // no scalar-load round trip per gather
+            const int cnt = (int)(end - kb < 64 ? end - kb : 64);
+            const int li = lane < cnt ? lane : cnt - 1;          // clamped: loads unconditional
+            const int d_col = col[kb + li];
+            const float d_val = val[kb + li];
+            for (int j = 0; j < cnt; j += U) {
+                float xv[U][NE];
 #pragma unroll
-            for (int q = 0; q < S; ++q)
-                if (ok[q]) {
-                    ldv<VW>(xs + cs[q], z + q * VW);
+                for (int u = 0; u < U; ++u) {
+                    const int jj = j + u < cnt ? j + u : cnt - 1;     // clamp: valid row
+                    const float *src = x + (int64_t)__builtin_amdgcn_readlane(d_col, jj) * ld_x;
 #pragma unroll
-                    for (int e = 0; e < VW; ++e)   // self * 0: keeps -0.0, inf/NaN -> NaN (p.mul_(0))
-                        z[q * VW + e] *= 0.f;
+                    for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xv[u] + q * VW);
                 }
-        }
+                if (kb == beg && j == 0) {
+                    // self * 0 (the first entry is the node itself): keeps -0.0, inf/NaN -> NaN
 #pragma unroll
-        for (int e = 0; e < NE; ++e) acc[e] = z[e];
-        // U independent gathers in flight, then in-order accumulation (the exact mode's order)
-        constexpr int U = SPL >= 4 ? 4 : 8;
-        int64_t k = beg;
-        for (; k < end; k += U) {
-            float xv[U][NE];
+                    for (int e = 0; e < NE; ++e) { z[e] = xv[0][e] * 0.f; acc[e] = z[e]; }
+                }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool have = k + u < end;                 // wave-uniform
-                const float *src = x + (int64_t)col[have ? k + u : beg] * ld_x;
+                for (int u = 0; u < U; ++u)
+                    if (j + u < cnt) {
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_val), j + u));
 #pragma unroll
-                for (int q = 0; q < S; ++q) {
-                    if (ok[q] && have) ldv<VW>(src + cs[q], xv[u] + q * VW);
-                    else {
-#pragma unroll
-                        for (int e = 0; e < VW; ++e) xv[u][q * VW + e] = 0.f;
+                        for (int e = 0; e < NE; ++e) acc[e] = axpy<EXACT>(w, xv[u][e], acc[e]);
                     }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (k + u < end) {
-                    const float w = val[k + u];
-#pragma unroll
-                    for (int e = 0; e < NE; ++e) acc[e] = axpy<EXACT>(w, xv[u][e], acc[e]);
-                }
             }
         }
         // update_models: p.mul_(0.); p.add_(new)  ->  z + acc   (AVERAGE_ONLY: acc)
@@ -799,7 +792,8 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
                         int mode, void *stream) {
     if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
     const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
-    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
+    const int low_degree = (mode & NIIDMIX_FLAG_LOW_DEGREE) ? 1 : 0;
+    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE);
     if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
         return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
     if (n_rows == 0 || p == 0) return NIIDMIX_OK;
@@ -818,13 +812,17 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     const int64_t n_row_groups = (n_rows + 3) / 4;
     const int64_t n_items = n_row_groups * ((n_chunks + 7) / 8) * 8;
     const dim3 grid((unsigned)grid_for(n_items)), block(256);
-#define NIIDMIX_CSR(E, V, S) hipLaunchKernelGGL((k_mix_csr<E, V, S>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only)
-#define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR(E, V, 4); else NIIDMIX_CSR(E, V, 1); } while (0)
+    // gathers in flight per batch: 4 when the caller flags a low-degree graph (ring, grid), else 8
+    const bool lowdeg = low_degree != 0;
+#define NIIDMIX_CSR(E, V, S, UU) hipLaunchKernelGGL((k_mix_csr<E, V, S, UU>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only)
+#define NIIDMIX_CSR_U(E, V, S) do { if (lowdeg) NIIDMIX_CSR(E, V, S, 4); else NIIDMIX_CSR(E, V, S, 8); } while (0)
+#define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR_U(E, V, 4); else NIIDMIX_CSR_U(E, V, 1); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) {
         if (vw == 4) NIIDMIX_CSR_S(true, 4); else if (vw == 2) NIIDMIX_CSR_S(true, 2); else NIIDMIX_CSR_S(true, 1);
     } else {
         if (vw == 4) NIIDMIX_CSR_S(false, 4); else if (vw == 2) NIIDMIX_CSR_S(false, 2); else NIIDMIX_CSR_S(false, 1);
     }
+#undef NIIDMIX_CSR_U
 #undef NIIDMIX_CSR_S
 #undef NIIDMIX_CSR
     return check_launch("k_mix_csr");

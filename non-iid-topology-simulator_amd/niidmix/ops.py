@@ -22,6 +22,7 @@ from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
 AVERAGE_ONLY = 2
+LOW_DEGREE = 4
 
 
 def _stream(t):
@@ -237,10 +238,11 @@ class Mixer:
         if out is None:
             out = torch.empty((self.n, x.shape[1]), dtype=torch.float32, device=x.device)
         k = kernel or self.kernel_for(mode, x, out)
+        hint = LOW_DEGREE if self.csr.nnz <= 4 * max(self.n, 1) else 0
         if k == "csr-exact":
-            mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT)
+            mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT | hint)
         elif k == "csr-fast":
-            mix_csr(x, self.row_ptr, self.col, self.val, out, FAST)
+            mix_csr(x, self.row_ptr, self.col, self.val, out, FAST | hint)
         elif k in ("staged-exact", "staged-fast"):
             _req(self.staged is not None, f"no staged plan: {self.staged_reason}")
             mix_staged(x, self.s_blk_ptr, self.s_blk_rows, self.s_src_ptr, self.s_src_rows,

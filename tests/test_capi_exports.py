@@ -42,7 +42,7 @@ def test_argument_errors_without_gpu():
     assert rc == _lib.EINVAL and b"null" in L.niidmix_last_error()
     rc = L.niidmix_mix_csr_f32(16, 4, 16, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EALIAS
-    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 7, None)
+    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 9, None)
     assert rc == _lib.EINVAL
     rc = L.niidmix_mix_csr_f32(16, 2, 1024, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EINVAL        # ld < p

@@ -156,3 +156,28 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
     b = run("oracle")
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def test_consensus_distance_event(gpu, tmp_path):
+    """The GPU consensus-distance event has the reference's schema and statistics."""
+    from niidmix import logger as nl
+    torch.manual_seed(3)
+    nodes = [{"rank": i, "model": torch.nn.Linear(50, 7)} for i in range(12)]
+    ev = nl.consensus_distance_event({"nodes": nodes, "step": 4})
+    d, norm = nl.reference_statistics([n["model"] for n in nodes])
+    import statistics
+    g = ev["distance_to_center"]["global"]
+    np.testing.assert_allclose(g["avg"], statistics.mean(d), rtol=1e-5)
+    np.testing.assert_allclose(g["max"], max(d), rtol=1e-5)
+    np.testing.assert_allclose(g["min"], min(d), rtol=1e-5)
+    np.testing.assert_allclose(g["std"], statistics.stdev(d), rtol=1e-4)
+    np.testing.assert_allclose(ev["center"]["norm"], norm, rtol=1e-5)
+    assert ev["type"] == "consensus-distance" and ev["step"] == 4
+
+    class L:
+        global_events = str(tmp_path / "global.jsonlines")
+    nl.install(L)
+    L().log_consensus_distance({"nodes": nodes, "step": 5})
+    import json
+    line = json.loads(open(L.global_events).read().strip())
+    assert line["step"] == 5 and "distance_to_center" in line

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/s16_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/s16_pytest.log; [ $rc -ge 1 ] && { grep -E "Error|assert|FAILED" gpurun_out/s16_pytest.log | head -20; exit $rc; }
+for a in "--config ring100 --steps 200" "--config ring100 --steps 200 --kernel csr-exact" "--steps 5 --kernel csr-exact" "--steps 5 --kernel csr-fast" "--steps 20"; do
+  timeout -k 10 200 python bench.py --no-cpu-baseline $a > gpurun_out/s16_b.json 2>gpurun_out/s16_b.err || { tail -5 gpurun_out/s16_b.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/s16_b.json')); print(d['config']['workload'][:20], d['config']['kernel'], d['config']['hipgraph'], d['ms_per_step'], d['value'], d['roofline']['achieved'], d['roofline']['frac'])"
+done
