@@ -65,6 +65,12 @@ __device__ __forceinline__ int wave_id() {
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
+__device__ __forceinline__ float4 ld4_nt(const float *p) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 __device__ __forceinline__ void st4_nt(float *p, float4 v) {
     __builtin_nontemporal_store(v.x, p + 0);
     __builtin_nontemporal_store(v.y, p + 1);
@@ -259,7 +265,7 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
     }
 }
 
-template <int WAVES, int RPW, int G, int OCC, int RW, bool PERSIST>
+template <int WAVES, int RPW, int G, int OCC, int RW, int FL>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
@@ -267,6 +273,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
+    constexpr bool PERSIST = (FL & 1) != 0;   // resident grid walking the items
+    constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
     __shared__ float4 red[G][WAVES][kWave];
     __shared__ float4 tot[G][kWave];
     const int wave = wave_id();
@@ -292,7 +300,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
             v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (wave + WAVES * r < M) {
                 const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-                if (act) v[r] = ld4(xc + row * ld_x + lo);
+                if (act) v[r] = NTL ? ld4_nt(xc + row * ld_x + lo) : ld4(xc + row * ld_x + lo);
             }
         }
         float4 rv[RW > 0 ? RW : 1];
@@ -710,11 +718,11 @@ bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) 
     return a < b + b_elems && b < a + a_elems;
 }
 
-template <int WAVES, int RPW, int G, int OCC, int RW, bool PERSIST>
+template <int WAVES, int RPW, int G, int OCC, int RW, int FL>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     int64_t grid = grid_for(n_items);
-    if (PERSIST) {
+    if (FL & 1) {
         // one resident wave of blocks, each walking items t, t+grid, ... (grid % 8 == 0 keeps the
         // XCD mapping); residency from the occupancy query, cached per instantiation
         static int blocks_per_cu = 0, n_cu = 0;
@@ -723,33 +731,33 @@ void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &blocks_per_cu, k_mix_clique<WAVES, RPW, G, OCC, RW, PERSIST>, WAVES * 64, 0);
+                &blocks_per_cu, k_mix_clique<WAVES, RPW, G, OCC, RW, FL>, WAVES * 64, 0);
             if (blocks_per_cu < 1) blocks_per_cu = 1;
         }
         const int64_t resident = ((int64_t)blocks_per_cu * n_cu + 7) / 8 * 8;
         if (resident < grid) grid = resident;
     }
-    hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, PERSIST>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
                        pl->res_val, n_items);
 }
 
-template <int WAVES, int RPW, int OCC, int RW, bool PERSIST>
+template <int WAVES, int RPW, int OCC, int RW, int FL>
 int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                     const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     switch (pl->n_groups) {
-        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, PERSIST>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, PERSIST>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, PERSIST>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, PERSIST>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
     return check_launch("k_mix_clique");
 }
 
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
-// targets, RW = residual rows prefetched per wave, PERSIST = resident grid walking the items.
+// targets, RW = residual rows prefetched per wave, FL = flags (1 persistent grid, 2 nt loads).
 // NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<onebar> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                         const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
@@ -772,9 +780,10 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 #define NIIDMIX_TILE(W, R, O, RWV, OB) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB) return launch_clique_g<W, R, O, RWV, OB>(x, ld_x, y, ld_y, p, pl, n_items, s)
     NIIDMIX_TILE(8, 2, 8, 0, 0); NIIDMIX_TILE(8, 4, 8, 0, 0); NIIDMIX_TILE(16, 4, 8, 0, 0);
     NIIDMIX_TILE(16, 7, 8, 0, 0); NIIDMIX_TILE(16, 8, 4, 0, 0); NIIDMIX_TILE(16, 16, 4, 0, 0);
-    // tuning alternatives (NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<persistent>)
+    // tuning alternatives (NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>, flags: 1 =
+    // persistent grid, 2 = non-temporal member loads)
     NIIDMIX_TILE(8, 13, 4, 0, 0); NIIDMIX_TILE(8, 13, 4, 2, 0); NIIDMIX_TILE(8, 13, 4, 2, 1);
-    NIIDMIX_TILE(16, 7, 8, 2, 0);
+    NIIDMIX_TILE(16, 7, 8, 2, 0); NIIDMIX_TILE(16, 7, 8, 0, 2); NIIDMIX_TILE(8, 13, 4, 0, 2);
 #undef NIIDMIX_TILE
     return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%d", waves, rpw, occ, rw, ob);
 }

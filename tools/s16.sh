@@ -6,3 +6,4 @@ for a in "--config ring100 --steps 200" "--config ring100 --steps 200 --kernel c
   timeout -k 10 200 python bench.py --no-cpu-baseline $a > gpurun_out/s16_b.json 2>gpurun_out/s16_b.err || { tail -5 gpurun_out/s16_b.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/s16_b.json')); print(d['config']['workload'][:20], d['config']['kernel'], d['config']['hipgraph'], d['ms_per_step'], d['value'], d['roofline']['achieved'], d['roofline']['frac'])"
 done
+timeout -k 10 400 python tools/tune_inproc.py --reps 3 --variant def::clique --variant nt16:NIIDMIX_CLIQUE_TILE=16x7x8x0x2:clique --variant b8:NIIDMIX_CLIQUE_TILE=8x13x4x0x0:clique --variant nt8:NIIDMIX_CLIQUE_TILE=8x13x4x0x2:clique
