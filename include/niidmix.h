@@ -140,6 +140,36 @@ typedef struct niidmix_staged_plan {
 int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                            const niidmix_staged_plan *plan, int mode, void *stream);
 
+/* Merged-order row tiles, exact or fast: the same result as niidmix_mix_csr_f32 (bit for bit in
+ * NIIDMIX_MODE_EXACT: every row keeps its own operand order — self, then edges[rank] in list order,
+ * d_sgd.py:105-106 — and its own roundings), computed so that rows sharing sources share the loads.
+ * Output rows are cut into tiles of rt rows (e.g. parts of a clique).  Each tile has one merged list
+ * of positions such that every row's entry list (self excluded) is a subsequence of it; a position
+ * names a source row, the tile rows that take it (mask) and their weights.  Built on the host by
+ * niidmix.tile.build_tile_plan.
+ *   n_sub      tiles;  rt  rows per tile: 8, 16 or 32
+ *   sub_ptr    [n_sub+1] int64 offsets into the position arrays
+ *   sub_rows   [n_sub*rt] int32 output rows, -1 for an unused slot
+ *   sub_wself  [n_sub*rt] fp32 W[r, r] of each tile row (its first CSR entry)
+ *   pos_src    [L] int32 source row of every position
+ *   pos_mask   [L] uint32: bit r set when tile row r takes the position (unused slots: set)
+ *   pos_w      [L*rt] fp32 weight W[src, row] per tile row (0 where the row skips the position)
+ * mode: NIIDMIX_MODE_EXACT / _FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY. */
+typedef struct niidmix_tile_plan {
+    int64_t n_sub;
+    int32_t rt;
+    int32_t reserved;
+    const int64_t *sub_ptr;
+    const int32_t *sub_rows;
+    const float *sub_wself;
+    const int32_t *pos_src;
+    const uint32_t *pos_mask;
+    const float *pos_w;
+} niidmix_tile_plan;
+
+int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                         const niidmix_tile_plan *plan, int mode, void *stream);
+
 /* Dense mixing Y = W^T X on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), for topologies dense
  * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).
  *   w  [n, n] fp32 row-major, w[src*n + dst] = W[src, dst] — the reference's topology['weights']

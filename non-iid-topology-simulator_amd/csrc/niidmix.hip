@@ -667,6 +667,129 @@ __global__ __launch_bounds__(256) void k_mix_staged(
 }
 
 // ----------------------------------------------------------------------------------------------
+// Merged-order row tiles (exact and fast).  The exact rule fixes every row's operand order (self,
+// then edges[rank] in list order), so rows cannot share partial sums — but they can share LOADS.
+// A tile is RT output rows (e.g. part of a clique) whose entry lists (self excluded) are all
+// subsequences of one merged position list (host: niidmix.tile, majority merge; a source that the
+// rows order differently appears more than once).  One wave owns (tile, column chunk) and holds
+// the RT rows' accumulators in registers; per position it loads the source row's columns ONCE and
+// applies them to every tile row that takes the position (mask bit), each row still in its own
+// list order, so exact mode stays bit-identical to k_mix_csr.  Work per position is RT*NE
+// mul+add per lane for one NE-column load: VALU-bound, not gather-bound.  Weights come in by
+// scalar loads (uniform per position), the source row / mask lane-parallel by v_readlane.  A
+// position every row takes (mask == FULL) skips the per-row select.
+template <bool EXACT, int VW, int NE, int RT>
+__global__ __launch_bounds__(256) void k_mix_tile(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int64_t n_sub, const int64_t *__restrict__ sub_ptr, const int32_t *__restrict__ sub_rows,
+    const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_src,
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w,
+    int64_t n_sub_groups, int64_t n_items, int avg_only) {
+    constexpr int S = NE / VW;                  // slots per lane
+    constexpr int64_t CW = 64 * NE;             // columns per work item
+    constexpr uint32_t FULL = RT == 32 ? 0xffffffffu : ((1u << RT) - 1u);
+    constexpr int D = 4;                        // positions whose loads are in flight together
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t chunk = (local / n_sub_groups) * 8 + xcd;
+        const int64_t sub = (local % n_sub_groups) * 4 + wave;
+        const int64_t c0 = chunk * CW;
+        if (sub >= n_sub || c0 >= p) continue;  // wave-uniform
+        int64_t cs[S];
+        bool ok[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const int64_t cq = c0 + VW * lane + 64 * VW * q;
+            ok[q] = cq < p;
+            cs[q] = ok[q] ? cq : c0;
+        }
+        const int li = lane < RT ? lane : RT - 1;
+        const int d_row = sub_rows[sub * RT + li];
+        const float d_ws = sub_wself[sub * RT + li];
+        float acc[RT][NE];
+        // first entry of every row: the node itself (acc = x*0; acc += w_self*x)
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+            const int row = __builtin_amdgcn_readlane(d_row, r);
+            const float *src = x + (int64_t)(row < 0 ? 0 : row) * ld_x;
+            float xs[NE];
+#pragma unroll
+            for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xs + q * VW);
+            const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
+#pragma unroll
+            for (int e = 0; e < NE; ++e) acc[r][e] = axpy<EXACT>(ws, xs[e], xs[e] * 0.f);
+        }
+        const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
+        for (int64_t kb = beg; kb < end; kb += 64) {
+            const int cnt = (int)(end - kb < 64 ? end - kb : 64);
+            const int lj = lane < cnt ? lane : cnt - 1;
+            const int d_src = pos_src[kb + lj];
+            const int d_mask = (int)pos_mask[kb + lj];
+            for (int j = 0; j < cnt; j += D) {
+                float xv[D][NE];
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    const int jj = j + u < cnt ? j + u : cnt - 1;     // clamped: loads unconditional
+                    const float *src = x + (int64_t)__builtin_amdgcn_readlane(d_src, jj) * ld_x;
+#pragma unroll
+                    for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xv[u] + q * VW);
+                }
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    if (j + u >= cnt) break;
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                    const float *wp = pos_w + (kb + j + u) * RT;
+                    if (m == FULL) {
+#pragma unroll
+                        for (int r = 0; r < RT; ++r) {
+                            const float w = wp[r];
+#pragma unroll
+                            for (int e = 0; e < NE; ++e) acc[r][e] = axpy<EXACT>(w, xv[u][e], acc[r][e]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < RT; ++r) {
+                            const float w = wp[r];
+                            const bool take = (m >> r) & 1u;
+#pragma unroll
+                            for (int e = 0; e < NE; ++e) {
+                                const float v = axpy<EXACT>(w, xv[u][e], acc[r][e]);
+                                acc[r][e] = take ? v : acc[r][e];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        // update_models: z + acc with z = x_self*0 (the self row is re-read: L2-resident, every
+        // position load of the tile's clique touched it) — saves RT*NE registers
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+            const int row = __builtin_amdgcn_readlane(d_row, r);
+            if (row < 0) continue;                                  // wave-uniform
+            float o[NE];
+            if (avg_only) {
+#pragma unroll
+                for (int e = 0; e < NE; ++e) o[e] = acc[r][e];
+            } else {
+                float xs[NE];
+#pragma unroll
+                for (int q = 0; q < S; ++q) ldv<VW>(x + (int64_t)row * ld_x + cs[q], xs + q * VW);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) o[e] = xs[e] * 0.f + acc[r][e];
+            }
+            float *dst = y + (int64_t)row * ld_y;
+#pragma unroll
+            for (int q = 0; q < S; ++q)
+                if (ok[q]) stv_nt<VW>(dst + cs[q], o + q * VW);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Uniform average over rows (model/__init__.py:17-24 with weights=None): one lane per column,
 // left-to-right over rows.  EXACT: mean = fl(...fl(fl(x0*0) + fl(w x0)) + ...), w = fp32(1/n).
 template <bool EXACT>
@@ -900,6 +1023,47 @@ int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     else                            { if (vpl == 2) NIIDMIX_STAGED(false, 2); else NIIDMIX_STAGED(false, 1); }
 #undef NIIDMIX_STAGED
     return check_launch("k_mix_staged");
+}
+
+int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                         const niidmix_tile_plan *plan, int mode, void *stream) {
+    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (p < 0 || plan->n_sub < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (plan->rt != 8 && plan->rt != 16 && plan->rt != 32)
+        return set_error(NIIDMIX_EUNSUPPORTED, "tile of %d rows (8, 16 or 32 supported)", plan->rt);
+    if (plan->n_sub == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !plan->sub_ptr || !plan->sub_rows || !plan->sub_wself || !plan->pos_src ||
+        !plan->pos_mask || !plan->pos_w)
+        return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    // columns per lane: 4 for 8- and 16-row tiles, 2 for 32-row tiles (register budget);
+    // NIIDMIX_TILE_NE=2|4 overrides (tuning)
+    int ne = plan->rt == 32 ? 2 : 4;
+    if (const char *e = getenv("NIIDMIX_TILE_NE")) { const int v = atoi(e); if (v == 2 || v == 4) ne = v; }
+    int vw = (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
+    if (ne == 4 && vw == 2 && p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && (align & 15) == 0) vw = 4;
+    const int64_t cw = 64 * ne;
+    const int64_t n_chunks = (p + cw - 1) / cw;
+    const int64_t n_sub_groups = (plan->n_sub + 3) / 4;
+    const int64_t n_items = n_sub_groups * ((n_chunks + 7) / 8) * 8;
+    const dim3 grid((unsigned)grid_for(n_items)), block(256);
+#define NIIDMIX_TILEK(E, V, N, R) hipLaunchKernelGGL((k_mix_tile<E, V, N, R>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_sub, plan->sub_ptr, plan->sub_rows, plan->sub_wself, plan->pos_src, plan->pos_mask, plan->pos_w, n_sub_groups, n_items, avg_only)
+#define NIIDMIX_TILE_V(E, N, R) do { if (vw == 4) NIIDMIX_TILEK(E, 4, 4, R); else if (vw == 2) NIIDMIX_TILEK(E, 2, N, R); else NIIDMIX_TILEK(E, 1, N, R); } while (0)
+#define NIIDMIX_TILE_N(E, R) do { if (ne == 4) NIIDMIX_TILE_V(E, 4, R); else NIIDMIX_TILE_V(E, 2, R); } while (0)
+#define NIIDMIX_TILE_R(E) do { if (plan->rt == 8) NIIDMIX_TILE_N(E, 8); else if (plan->rt == 16) NIIDMIX_TILE_N(E, 16); else NIIDMIX_TILE_N(E, 32); } while (0)
+    if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_TILE_R(true); else NIIDMIX_TILE_R(false);
+#undef NIIDMIX_TILE_R
+#undef NIIDMIX_TILE_N
+#undef NIIDMIX_TILE_V
+#undef NIIDMIX_TILEK
+    return check_launch("k_mix_tile");
 }
 
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,

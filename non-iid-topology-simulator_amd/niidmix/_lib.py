@@ -35,6 +35,12 @@ class StagedPlanC(ctypes.Structure):
                 ("src_ptr", _vp), ("src_rows", _vp), ("row_ptr", _vp), ("scol", _vp), ("val", _vp)]
 
 
+class TilePlanC(ctypes.Structure):
+    """Mirror of struct niidmix_tile_plan (include/niidmix.h)."""
+    _fields_ = [("n_sub", _i64), ("rt", _i32), ("reserved", _i32), ("sub_ptr", _vp), ("sub_rows", _vp),
+                ("sub_wself", _vp), ("pos_src", _vp), ("pos_mask", _vp), ("pos_w", _vp)]
+
+
 # every symbol include/niidmix.h declares, with its ctypes signature
 SIGNATURES = {
     "niidmix_abi_version": (ctypes.c_int, []),
@@ -45,6 +51,8 @@ SIGNATURES = {
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_staged_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(StagedPlanC), ctypes.c_int, _vp]),
+    "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+                                            ctypes.POINTER(TilePlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_copy2d_async": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp]),

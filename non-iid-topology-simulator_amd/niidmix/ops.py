@@ -11,6 +11,7 @@ RuntimeError (TORCH_CHECK-style) on bad arguments.  They accept HIP tensors only
 implementation and no fallback.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -18,6 +19,7 @@ import torch
 from . import _lib
 from .factor import build_clique_plan
 from .staged import build_staged_plan
+from .tile import build_tile_plan
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -143,6 +145,29 @@ def mix_staged(x: torch.Tensor, blk_ptr: torch.Tensor, blk_rows: torch.Tensor,
     _lib.check(rc, "niidmix::mix_staged")
 
 
+@torch.library.custom_op("niidmix::mix_tile", mutates_args=("out",))
+def mix_tile(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
+             sub_wself: torch.Tensor, pos_src: torch.Tensor, pos_mask: torch.Tensor,
+             pos_w: torch.Tensor, out: torch.Tensor, rt: int, mode: int) -> None:
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    dev = x.device
+    t = sub_ptr.numel() - 1
+    _vec("sub_ptr", sub_ptr, torch.int64, dev)
+    _vec("sub_rows", sub_rows, torch.int32, dev, t * rt)
+    _vec("sub_wself", sub_wself, torch.float32, dev, t * rt)
+    _vec("pos_src", pos_src, torch.int32, dev)
+    _vec("pos_mask", pos_mask, torch.int32, dev, pos_src.numel())      # uint32 bits
+    _vec("pos_w", pos_w, torch.float32, dev, pos_src.numel() * rt)
+    _no_overlap(x, out)
+    plan = _lib.TilePlanC(t, int(rt), 0, sub_ptr.data_ptr(), sub_rows.data_ptr(),
+                          sub_wself.data_ptr(), pos_src.data_ptr(), pos_mask.data_ptr(),
+                          pos_w.data_ptr())
+    rc = _lib.lib.niidmix_mix_tile_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
+                                       ctypes.byref(plan), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_tile")
+
+
 @torch.library.custom_op("niidmix::mix_dense", mutates_args=("out",))
 def mix_dense(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
     _slab("x", x)
@@ -219,6 +244,20 @@ class Mixer:
             self.s_src_ptr = torch.from_numpy(sp.src_ptr).to(dev)
             self.s_src_rows = torch.from_numpy(sp.src_rows).to(dev)
             self.s_scol = torch.from_numpy(sp.scol).to(dev)
+        # merged-order row tiles (exact mode's fast path): only worth building when rows read many
+        # sources (avg degree >= 8); NIIDMIX_TILE_RT=8|16|32 picks the tile height
+        self.tile, self.tile_reason = (None, "average degree < 8")
+        if csr.nnz >= 9 * max(csr.n, 1):
+            rt = int(os.environ.get("NIIDMIX_TILE_RT", "16"))
+            self.tile, self.tile_reason = build_tile_plan(csr, cliques, rt)
+        if self.tile is not None:
+            tp = self.tile
+            self.t_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+            self.t_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+            self.t_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+            self.t_pos_src = torch.from_numpy(tp.pos_src).to(dev)
+            self.t_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+            self.t_pos_w = torch.from_numpy(tp.pos_w).to(dev)
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
@@ -248,6 +287,11 @@ class Mixer:
             mix_staged(x, self.s_blk_ptr, self.s_blk_rows, self.s_src_ptr, self.s_src_rows,
                        self.row_ptr, self.s_scol, self.val, out, self.staged.max_src,
                        EXACT if k == "staged-exact" else FAST)
+        elif k in ("tile-exact", "tile-fast"):
+            _req(self.tile is not None, f"no tile plan: {self.tile_reason}")
+            mix_tile(x, self.t_sub_ptr, self.t_sub_rows, self.t_sub_wself, self.t_pos_src,
+                     self.t_pos_mask, self.t_pos_w, out, self.tile.rt,
+                     EXACT if k == "tile-exact" else FAST)
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,

@@ -56,5 +56,14 @@ def test_argument_errors_without_gpu():
     sp = _lib.StagedPlanC(1, 300, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_staged_f32(16, 4, 1024, 4, 4, ctypes.byref(sp), 0, None)
     assert rc == _lib.EUNSUPPORTED   # more than 256 staged source rows
+    tp = _lib.TilePlanC(1, 12, 0, 8, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 0, None)
+    assert rc == _lib.EUNSUPPORTED   # tile height 12
+    tp = _lib.TilePlanC(1, 16, 0, None, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 0, None)
+    assert rc == _lib.EINVAL         # null sub_ptr
+    tp = _lib.TilePlanC(1, 16, 0, 8, 8, 8, 8, 8, 8)
+    assert L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 9, None) == _lib.EINVAL
+    assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
     rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
     assert rc == _lib.EINVAL

@@ -27,19 +27,21 @@ def _mixer(g, dev, **kw):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact"])
+@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact", "tile-exact"])
 def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     m = _mixer(g, gpu)
     if kernel == "staged-exact" and m.staged is None:
         pytest.skip(f"no staged plan: {m.staged_reason}")
+    if kernel == "tile-exact" and m.tile is None:
+        m = _tile_mixer(g, gpu, 8)
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel=kernel).cpu().numpy()
     assert oracle_mod.bitwise_equal(y, g["y"]), name
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "staged-fast"])
+@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "staged-fast", "tile-fast"])
 def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     if not np.all(np.isfinite(g["x"])):
@@ -50,11 +52,48 @@ def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
         pytest.skip(f"no clique plan ({m.plan_reason}) or p % 4")
     if kernel == "staged-fast" and m.staged is None:
         pytest.skip(f"no staged plan ({m.staged_reason})")
+    if kernel == "tile-fast" and m.tile is None:
+        m = _tile_mixer(g, gpu, 16)
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel=kernel).cpu().numpy()
     bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
     ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
     assert ok, f"{name}/{kernel}: worst {worst:.3g}"
+
+
+def _tile_mixer(g, dev, rt):
+    """A Mixer with a tile plan of height rt even for low-degree topologies (tests only)."""
+    from niidmix import tile
+    m = _mixer(g, dev)
+    tp, why = tile.build_tile_plan(m.csr, g.get("cliques"), rt)
+    assert tp is not None, why
+    m.tile = tp
+    m.t_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+    m.t_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+    m.t_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+    m.t_pos_src = torch.from_numpy(tp.pos_src).to(dev)
+    m.t_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+    m.t_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+    return m
+
+
+@pytest.mark.parametrize("rt", [8, 16, 32])
+@pytest.mark.parametrize("name", ["dcliques1000_fc_p64", "dcliques300_fc_p37", "fc64_p33",
+                                  "nonfinite_ring8_p16", "n2_ring_linear7850", "ring100_p257"])
+def test_tile_exact_heights_bitwise(name, rt, gpu, oracle_mod):
+    """Every tile height (8/16/32 rows; vector widths follow p) is bit-identical to the reference,
+    including the average-only flag (setup.model.average alone)."""
+    g = load_golden(name)
+    m = _tile_mixer(g, gpu, rt)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"]), (name, rt)
+    ops = _ops()
+    out = torch.empty_like(x)
+    ops.mix_tile(x, m.t_sub_ptr, m.t_sub_rows, m.t_sub_wself, m.t_pos_src, m.t_pos_mask,
+                 m.t_pos_w, out, rt, ops.EXACT | ops.AVERAGE_ONLY)
+    ref = oracle_mod.mix_exact_c(g["x"], g["row_ptr"], g["col"], g["val"], average_only=True)
+    assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref), (name, rt)
 
 
 def test_auto_kernel_choice(gpu):
@@ -90,7 +129,7 @@ def _windows(p, w=2048):
     return [(0, w), (p // 2 - w // 2, p // 2 + w // 2), (p - w, p)]
 
 
-@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact"])
+@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact", "tile-exact"])
 def test_full_size_exact_windows(kernel, gpu, oracle_mod):
     """BASELINE configs[2] at full size (N=1000 d-cliques, P=2^20): exact kernels are bit-identical
     to the oracle on sampled column windows (columns are independent)."""

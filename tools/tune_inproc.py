@@ -40,19 +40,39 @@ def main():
         name, env, kernel = v.split(":")
         envd = dict(kv.split("=") for kv in env.split(",") if kv)
         variants.append((name, envd, kernel))
+    mixers = {}
+
+    def mixer_for(envd):
+        rt = envd.get("NIIDMIX_TILE_RT")
+        if rt is None:
+            return m
+        if rt not in mixers:
+            saved = os.environ.get("NIIDMIX_TILE_RT")
+            os.environ["NIIDMIX_TILE_RT"] = rt
+            mixers[rt] = ops.Mixer(csr=csr, cliques=cl, device=dev)
+            if saved is None:
+                os.environ.pop("NIIDMIX_TILE_RT")
+            else:
+                os.environ["NIIDMIX_TILE_RT"] = saved
+            t = mixers[rt].tile
+            if t is not None:
+                print(f"tile rt={rt}: {t.n_sub} tiles, {t.n_pos} positions, density {t.density:.3f}")
+        return mixers[rt]
+
     res = {n: [] for n, _, _ in variants}
     res["copy"] = []
     for rep in range(a.reps):
         for name, envd, kernel in variants:
+            mm = mixer_for(envd)
             saved = {k: os.environ.get(k) for k in envd}
             os.environ.update(envd)
             for _ in range(3):
-                m(x, out=y, kernel=kernel)
+                mm(x, out=y, kernel=kernel)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             s.record()
             for _ in range(a.steps):
-                m(x, out=y, kernel=kernel)
+                mm(x, out=y, kernel=kernel)
             e.record()
             torch.cuda.synchronize()
             res[name].append(s.elapsed_time(e) / a.steps)
