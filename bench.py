@@ -26,6 +26,7 @@ is d-cliques over 1000*N nodes (see --interclique), cliques sharded whole across
 cross-shard edges' rows are exchanged over RCCL (xGMI) every round before the mixing kernel.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -69,6 +70,8 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident round (pinned [N,P] host slab -> H2D -> mix -> "
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
+    ap.add_argument("--ld-pad", type=int, default=0,
+                    help="single GPU: pad every slab row by this many floats (ld = P + pad)")
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
     return ap.parse_args()
@@ -104,17 +107,28 @@ def single_gpu_topology(cfg):
     raise ValueError(cfg)
 
 
-def stream_copy_probe(a, b, iters=10):
-    """Measured read+write ceiling on this GPU: torch copy_ of the same slab (2*bytes per copy)."""
-    b.copy_(a)
+def stream_copy_probe(numel, dev, iters=10):
+    """This GPU's own HBM copy ceiling: libniidmix's streaming copy (nt float4 loads + stores,
+    linear order) of a slab of the same size, 2*bytes per copy.  Boxes differ by up to ~20 %."""
+    from niidmix import _lib
+    numel -= numel % 4
+    a = torch.zeros(numel, device=dev)
+    b = torch.empty_like(a)
+    strm = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    def cp():
+        _lib.check(_lib.lib.niidmix_stream_copy_f32(a.data_ptr(), b.data_ptr(), numel, strm),
+                   "stream copy")
+    cp()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
     for _ in range(iters):
-        b.copy_(a)
+        cp()
     e.record()
     torch.cuda.synchronize()
-    return 2 * a.numel() * 4 * iters / (s.elapsed_time(e) / 1e3) / 1e9
+    del a, b
+    return 2 * numel * 4 * iters / (s.elapsed_time(e) / 1e3) / 1e9
 
 
 def e2e_rounds(mixer, n, p, dev, rounds=3):
@@ -235,8 +249,9 @@ def main():
         n_local = n_total = csr.n
         parallelism = "single GPU"
         gen = torch.Generator(device=dev).manual_seed(args.seed)
-        xa = torch.randn(n_local, p, device=dev, generator=gen)
-        xb = torch.empty_like(xa)
+        ld = p + args.ld_pad
+        xa = torch.randn(n_local, ld, device=dev, generator=gen)[:, :p]
+        xb = torch.empty(n_local, ld, device=dev)[:, :p]
         halo = 0
     else:
         from niidmix.shard import ShardedMixer
@@ -313,7 +328,7 @@ def main():
         region_s, launch_ms = tt.tolist()
     step_s = region_s / args.steps
     value = n_total * p * 4 / step_s / 1e9
-    copy_gbs = stream_copy_probe(xa, xb)
+    copy_gbs = stream_copy_probe(n_local * p, dev)
 
     if rank == 0:
         if kernel == "dense":
@@ -344,7 +359,9 @@ def main():
                        "mode": mode, "parallelism": parallelism,
                        "launch_ms": round(launch_ms, 4), "halo_rows_rank0": halo,
                        "hipgraph": graph is not None,
-                       "stream_copy_GBs": round(copy_gbs, 1)},
+                       "stream_copy_GBs": round(copy_gbs, 1),
+                       "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
+                                               if roof["unit"] == "GB/s" else None)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -154,6 +154,7 @@ int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  *   pos_src    [L] int32 source row of every position
  *   pos_mask   [L] uint32: bit r set when tile row r takes the position (unused slots: set)
  *   pos_w      [L*rt] fp32 weight W[src, row] per tile row (0 where the row skips the position)
+ *   (pos_* must be valid device pointers even when L == 0; they are read only inside sub_ptr ranges)
  * mode: NIIDMIX_MODE_EXACT / _FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY. */
 typedef struct niidmix_tile_plan {
     int64_t n_sub;
@@ -192,6 +193,12 @@ int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
  * 2 = device->device.  Stream-ordered; host memory must be pinned for the copy to be asynchronous. */
 int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,
                          int64_t width_bytes, int64_t rows, int kind, void *stream);
+
+/* Streaming copy y[0:n] = x[0:n] (fp32, n % 4 == 0, 16-B aligned, no overlap) with non-temporal
+ * loads and stores, one float4 per thread in linear order.  Not part of the reference's path: a
+ * measurement primitive that gives bench.py this GPU's own HBM copy ceiling to report the mixing
+ * kernel against (MI355X boxes differ by up to ~20 % in achievable HBM bandwidth). */
+int niidmix_stream_copy_f32(const float *x, float *y, int64_t n, void *stream);
 
 #ifdef __cplusplus
 }

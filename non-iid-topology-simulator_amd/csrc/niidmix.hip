@@ -790,6 +790,20 @@ __global__ __launch_bounds__(256) void k_mix_tile(
 }
 
 // ----------------------------------------------------------------------------------------------
+// Streaming copy ceiling (measurement primitive, not part of the mixing path): one float4 per
+// thread, non-temporal loads and stores, linear order — the access shape that measured fastest on
+// MI355X (tools/hbm_probe2.hip: ~6.6 TB/s), so bench.py can report the mixing kernel against this
+// box's own copy rate next to the 8 TB/s spec.
+__global__ __launch_bounds__(256) void k_stream_copy(const float *__restrict__ x, float *__restrict__ y,
+                                                     int64_t n4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n4)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const f4 *>(x) + i),
+                                    reinterpret_cast<f4 *>(y) + i);
+}
+
+// ----------------------------------------------------------------------------------------------
 // Uniform average over rows (model/__init__.py:17-24 with weights=None): one lane per column,
 // left-to-right over rows.  EXACT: mean = fl(...fl(fl(x0*0) + fl(w x0)) + ...), w = fp32(1/n).
 template <bool EXACT>
@@ -1130,6 +1144,21 @@ int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64
     if (e != hipSuccess) return set_error(NIIDMIX_EHIP, "hipMemcpy2DAsync: %s", hipGetErrorString(e));
     g_last_error[0] = '\0';
     return NIIDMIX_OK;
+}
+
+int niidmix_stream_copy_f32(const float *x, float *y, int64_t n, void *stream) {
+    if (n < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n == 0) return NIIDMIX_OK;
+    if (!x || !y) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (n % 4 != 0 || !aligned16(x) || !aligned16(y))
+        return set_error(NIIDMIX_EUNSUPPORTED, "stream copy needs n %% 4 == 0 and 16-B aligned buffers");
+    if ((x < y && x + n > y) || (y < x && y + n > x) || x == y)
+        return set_error(NIIDMIX_EALIAS, "x and y overlap");
+    const int64_t n4 = n / 4, blocks = (n4 + 255) / 256;
+    if (blocks > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "copy too large for one grid");
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, y, n4);
+    return check_launch("k_stream_copy");
 }
 
 }  // extern "C"

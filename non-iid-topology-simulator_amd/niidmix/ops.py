@@ -160,9 +160,12 @@ def mix_tile(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
     _vec("pos_mask", pos_mask, torch.int32, dev, pos_src.numel())      # uint32 bits
     _vec("pos_w", pos_w, torch.float32, dev, pos_src.numel() * rt)
     _no_overlap(x, out)
+    # a plan without positions (every row reads only itself, e.g. N = 1) still passes valid
+    # pointers: the C-ABI refuses NULL, and the kernel reads pos_* only inside sub_ptr ranges
+    some = sub_ptr.data_ptr()
     plan = _lib.TilePlanC(t, int(rt), 0, sub_ptr.data_ptr(), sub_rows.data_ptr(),
-                          sub_wself.data_ptr(), pos_src.data_ptr(), pos_mask.data_ptr(),
-                          pos_w.data_ptr())
+                          sub_wself.data_ptr(), pos_src.data_ptr() or some,
+                          pos_mask.data_ptr() or some, pos_w.data_ptr() or some)
     rc = _lib.lib.niidmix_mix_tile_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
                                        ctypes.byref(plan), int(mode), _stream(x))
     _lib.check(rc, "niidmix::mix_tile")

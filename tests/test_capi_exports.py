@@ -67,3 +67,7 @@ def test_argument_errors_without_gpu():
     assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
     rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
     assert rc == _lib.EINVAL
+    assert L.niidmix_stream_copy_f32(16, 1024, 6, None) == _lib.EUNSUPPORTED   # n % 4
+    assert L.niidmix_stream_copy_f32(16, 32, 8, None) == _lib.EALIAS
+    assert L.niidmix_stream_copy_f32(None, 32, 8, None) == _lib.EINVAL
+    assert L.niidmix_stream_copy_f32(16, 1024, 0, None) == _lib.OK

@@ -239,3 +239,17 @@ def test_fc1000_dense_and_factored(kernel, gpu, oracle_mod):
     bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
     ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
     assert ok, worst
+
+
+@pytest.mark.gpu
+def test_stream_copy(gpu):
+    """The bench's copy-ceiling primitive copies exactly (ragged tail of the last block included)."""
+    import ctypes
+    from niidmix import _lib
+    for n in (4, 1020, 1 << 20, (1 << 20) + 36):
+        a = torch.randn(n, device=gpu)
+        b = torch.zeros(n, device=gpu)
+        s = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+        _lib.check(_lib.lib.niidmix_stream_copy_f32(a.data_ptr(), b.data_ptr(), n, s))
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)

@@ -43,6 +43,16 @@ __global__ void copy_lin2_nt(const float4 *__restrict__ x, float4 *__restrict__ 
         for (int u = 0; u < 4; ++u) if (i + u * stride < n) __builtin_nontemporal_store(w[u], (f4 *)(y + i + u * stride));
     }
 }
+template <int U>
+__global__ __launch_bounds__(256) void copy_once(const float4 *__restrict__ x, float4 *__restrict__ y, size_t n) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    f4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) if (base + 256 * u < n) w[u] = *(const f4 *)(x + base + 256 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) if (base + 256 * u < n) __builtin_nontemporal_store(w[u], (f4 *)(y + base + 256 * u));
+}
 __global__ void read_lin(const float4 *__restrict__ x, float *__restrict__ out, size_t n) {
     float s = 0.f;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -55,14 +65,21 @@ __global__ void write_lin(float4 *__restrict__ y, size_t n) {
 }
 
 template <int WAVES, int RPW, int VPL, int NBAR = 0>
-__global__ __launch_bounds__(WAVES * 64) void copy_rows(const float *__restrict__ x, float *__restrict__ y, long ld, long p, int rows_per_clique, int n_cliques, long n_items) {
+__global__ __launch_bounds__(WAVES * 64) void copy_rows(const float *__restrict__ x, float *__restrict__ y, long ld, long p, int rows_per_clique, int n_cliques, long n_items, long sc = 0) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const long chunkw = 256 * VPL;
     for (long t = blockIdx.x; t < n_items; t += gridDim.x) {
-        const long xcd = t & 7, local = t >> 3;
-        const long chunk = (local / n_cliques) * 8 + xcd;
-        const int cq = (int)(local % n_cliques);
+        long chunk; int cq;
+        if (sc == 0) {
+            const long xcd = t & 7, local = t >> 3;
+            chunk = (local / n_cliques) * 8 + xcd;
+            cq = (int)(local % n_cliques);
+        } else {   // super-chunks of sc chunks; inside one, clique-major
+            const long per = sc * n_cliques, s0 = t / per, rem = t % per;
+            cq = (int)(rem / sc);
+            chunk = s0 * sc + rem % sc;
+        }
         if (chunk * chunkw >= p) continue;
         const float *xc = x + chunk * chunkw;
         float *yc = y + chunk * chunkw;
@@ -129,10 +146,13 @@ __global__ __launch_bounds__(256) void copy_rows_dw(const float *__restrict__ x,
 
 int main(int argc, char **argv) {
     const long N = argc > 1 ? atol(argv[1]) : 1000, P = argc > 2 ? atol(argv[2]) : (1 << 20);
-    const size_t n4 = (size_t)N * P / 4, bytes = (size_t)N * P * 4;
+    const long PAD = argc > 3 ? atol(argv[3]) : 0;      // row padding in floats (ld = P + PAD)
+    const long LD = P + PAD;
+    const size_t n4 = (size_t)N * P / 4, bytes = (size_t)N * P * 4, alloc = (size_t)N * LD * 4;
     float *x, *y, *o;
-    CK(hipMalloc(&x, bytes)); CK(hipMalloc(&y, bytes)); CK(hipMalloc(&o, 64));
-    CK(hipMemset(x, 0, bytes)); CK(hipMemset(y, 0, bytes));
+    CK(hipMalloc(&x, alloc)); CK(hipMalloc(&y, alloc)); CK(hipMalloc(&o, 64));
+    CK(hipMemset(x, 0, alloc)); CK(hipMemset(y, 0, alloc));
+    printf("N=%ld P=%ld ld=%ld\n", N, P, LD);
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     auto timeit = [&](const char *name, double moved, auto launch) {
         for (int i = 0; i < 3; ++i) launch();
@@ -154,25 +174,35 @@ int main(int argc, char **argv) {
     timeit("copy_lin_ntnt g65536", 2.0 * bytes, [&] { copy_lin_ntnt<<<65536, 256>>>((const float4 *)x, (float4 *)y, n4); });
     timeit("copy_lin2_nt g16384", 2.0 * bytes, [&] { copy_lin2_nt<<<16384, 256>>>((const float4 *)x, (float4 *)y, n4); });
     timeit("copy_lin2_nt g4096", 2.0 * bytes, [&] { copy_lin2_nt<<<4096, 256>>>((const float4 *)x, (float4 *)y, n4); });
+    timeit("copy_once U1", 2.0 * bytes, [&] { copy_once<1><<<(n4 + 255) / 256, 256>>>((const float4 *)x, (float4 *)y, n4); });
+    timeit("copy_once U2", 2.0 * bytes, [&] { copy_once<2><<<(n4 + 511) / 512, 256>>>((const float4 *)x, (float4 *)y, n4); });
+    timeit("copy_once U4", 2.0 * bytes, [&] { copy_once<4><<<(n4 + 1023) / 1024, 256>>>((const float4 *)x, (float4 *)y, n4); });
     timeit("read_lin g8192", 1.0 * bytes, [&] { read_lin<<<8192, 256>>>((const float4 *)x, o, n4); });
     timeit("write_lin g8192", 1.0 * bytes, [&] { write_lin<<<8192, 256>>>((float4 *)y, n4); });
     const int R = 100, C = (int)(N / R);
     {
         const long items = (long)C * (((P + 255) / 256 + 7) / 8) * 8;
-        timeit("copy_rows 16x7 c256", 2.0 * bytes, [&] { copy_rows<16, 7, 1><<<items, 1024>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 8x13 c256", 2.0 * bytes, [&] { copy_rows<8, 13, 1><<<items, 512>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 16x7 c256 bar1", 2.0 * bytes, [&] { copy_rows<16, 7, 1, 1><<<items, 1024>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 16x7 c256 bar2", 2.0 * bytes, [&] { copy_rows<16, 7, 1, 2><<<items, 1024>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 8x13 c256 bar1", 2.0 * bytes, [&] { copy_rows<8, 13, 1, 1><<<items, 512>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 8x13 c256 bar2", 2.0 * bytes, [&] { copy_rows<8, 13, 1, 2><<<items, 512>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 4x25 c256 bar2", 2.0 * bytes, [&] { copy_rows<4, 25, 1, 2><<<items, 256>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 4x25 c256", 2.0 * bytes, [&] { copy_rows<4, 25, 1><<<items, 256>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows_dw 100 c256", 2.0 * bytes, [&] { copy_rows_dw<100><<<items, 256>>>(x, y, P, P, C, items); });
+        timeit("copy_rows 16x7 c256", 2.0 * bytes, [&] { copy_rows<16, 7, 1><<<items, 1024>>>(x, y, LD, P, R, C, items); });
+        for (long sc : {64L, 256L, 1024L, 4096L}) {
+            char nm[64];
+            snprintf(nm, 64, "copy_rows 16x7 c256 sc%ld", sc);
+            timeit(nm, 2.0 * bytes, [&] { copy_rows<16, 7, 1><<<items, 1024>>>(x, y, LD, P, R, C, items, sc); });
+            snprintf(nm, 64, "copy_rows 8x13 c256 sc%ld", sc);
+            timeit(nm, 2.0 * bytes, [&] { copy_rows<8, 13, 1><<<items, 512>>>(x, y, LD, P, R, C, items, sc); });
+        }
+        timeit("copy_rows 8x13 c256", 2.0 * bytes, [&] { copy_rows<8, 13, 1><<<items, 512>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 16x7 c256 bar1", 2.0 * bytes, [&] { copy_rows<16, 7, 1, 1><<<items, 1024>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 16x7 c256 bar2", 2.0 * bytes, [&] { copy_rows<16, 7, 1, 2><<<items, 1024>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 8x13 c256 bar1", 2.0 * bytes, [&] { copy_rows<8, 13, 1, 1><<<items, 512>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 8x13 c256 bar2", 2.0 * bytes, [&] { copy_rows<8, 13, 1, 2><<<items, 512>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 4x25 c256 bar2", 2.0 * bytes, [&] { copy_rows<4, 25, 1, 2><<<items, 256>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 4x25 c256", 2.0 * bytes, [&] { copy_rows<4, 25, 1><<<items, 256>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows_dw 100 c256", 2.0 * bytes, [&] { copy_rows_dw<100><<<items, 256>>>(x, y, LD, P, C, items); });
     }
     {
         const long items = (long)C * (((P + 511) / 512 + 7) / 8) * 8;
-        timeit("copy_rows 16x7 c512", 2.0 * bytes, [&] { copy_rows<16, 7, 2><<<items, 1024>>>(x, y, P, P, R, C, items); });
-        timeit("copy_rows 8x13 c512", 2.0 * bytes, [&] { copy_rows<8, 13, 2><<<items, 512>>>(x, y, P, P, R, C, items); });
+        timeit("copy_rows 16x7 c512", 2.0 * bytes, [&] { copy_rows<16, 7, 2><<<items, 1024>>>(x, y, LD, P, R, C, items); });
+        timeit("copy_rows 8x13 c512", 2.0 * bytes, [&] { copy_rows<8, 13, 2><<<items, 512>>>(x, y, LD, P, R, C, items); });
     }
     return 0;
 }
