@@ -213,8 +213,9 @@ struct CliqueDesc {        // one work item's member descriptors, lane-parallel 
     int32_t m0, M;         // wave-uniform
     int row, grp, rb, re;  // per lane
     float cf[1 + G];
-    int rsrc;              // lane j < RW: j-th residual entry of this wave (source row, weight)
-    float rw;
+    int nres;              // wave-uniform: residual entries of this wave's members
+    int rsrc, rslot;       // lane j < RW: j-th residual entry of this wave (source row, member slot,
+    float rw;              //   weight)
 };
 
 template <int WAVES, int RPW, int G, int RW>
@@ -224,9 +225,7 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
                                                  const int32_t *__restrict__ member_row,
                                                  const int32_t *__restrict__ member_group,
                                                  const float *__restrict__ coef,
-                                                 const int32_t *__restrict__ res_ptr,
-                                                 const int32_t *__restrict__ res_col,
-                                                 const float *__restrict__ res_val) {
+                                                 const int32_t *__restrict__ res_ptr) {
     const int64_t local = t >> 3;
     const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
     const int32_t cq = (int32_t)(local % n_cliques);
@@ -245,23 +244,30 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
 #pragma unroll
         for (int g = 0; g <= G; ++g) d.cf[g] = coef[(int64_t)m * (1 + G) + g];
     }
-    d.rsrc = 0;
-    d.rw = 0.f;
-    if (RW > 0) {
-        int pre = 0, q_j = -1;
+}
+
+// Second descriptor step, issued AFTER the member-row loads so its latency hides under them: lane j
+// of the wave takes the wave's j-th residual entry (members in slot order, each member's entries in
+// res order) — its source row, weight and the member slot it belongs to.
+template <int RPW, int G, int RW>
+__device__ __forceinline__ void load_res_desc(CliqueDesc<G, RW> &d, int lane,
+                                              const int32_t *__restrict__ res_col,
+                                              const float *__restrict__ res_val) {
+    int pre = 0, q_j = -1, slot = 0;
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int rb = __builtin_amdgcn_readlane(d.rb, r);
-            const int cnt = __builtin_amdgcn_readlane(d.re, r) - rb;
-            if (lane >= pre && lane < pre + cnt) q_j = rb + lane - pre;
-            pre += cnt;
-        }
-        if (lane < RW && q_j >= 0) {
-            d.rsrc = res_col[q_j];
-            d.rw = res_val[q_j];
-        } else {
-            d.rsrc = __builtin_amdgcn_readlane(d.row, 0);
-        }
+    for (int r = 0; r < RPW; ++r) {
+        const int rb = __builtin_amdgcn_readlane(d.rb, r);
+        const int cnt = __builtin_amdgcn_readlane(d.re, r) - rb;
+        if (lane >= pre && lane < pre + cnt) { q_j = rb + lane - pre; slot = r; }
+        pre += cnt;
+    }
+    d.nres = pre;
+    d.rslot = slot;
+    d.rsrc = __builtin_amdgcn_readlane(d.row, 0);
+    d.rw = 0.f;
+    if (RW > 0 && lane < RW && q_j >= 0) {
+        d.rsrc = res_col[q_j];
+        d.rw = res_val[q_j];
     }
 }
 
@@ -273,18 +279,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
-    constexpr bool PERSIST = (FL & 1) != 0;   // resident grid walking the items
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
+    constexpr int RU = 2;                     // residual rows gathered per batch
     __shared__ float4 red[G][WAVES][kWave];
     __shared__ float4 tot[G][kWave];
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
-    CliqueDesc<G, RW> d;
-    int64_t t = blockIdx.x;
-    if (t < n_items)
+    {
+        const int64_t t = blockIdx.x;             // one work item per block (grid = n_items)
+        if (t >= n_items) return;
+        CliqueDesc<G, RW> d;
         load_clique_desc<WAVES, RPW, G, RW>(d, t, n_cliques, p, wave, lane, clique_ptr, member_row,
-                                            member_group, coef, res_ptr, res_col, res_val);
-    for (; t < n_items; t += gridDim.x) {
+                                            member_group, coef, res_ptr);
         const int64_t local = t >> 3;
         const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
         const bool act = chunk * kChunk + 4 * lane < p;
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         float *yc = y + chunk * kChunk;
         const unsigned lo = 4u * (unsigned)lane;
 
-        // 1. member rows (and this wave's first RW residual source rows) -> registers
+        // 1. member rows -> registers, all loads in flight before the first use
         float4 v[RPW];
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -303,18 +309,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 if (act) v[r] = NTL ? ld4_nt(xc + row * ld_x + lo) : ld4(xc + row * ld_x + lo);
             }
         }
-        float4 rv[RW > 0 ? RW : 1];
-#pragma unroll
-        for (int j = 0; j < RW; ++j) {
-            const int64_t row = __builtin_amdgcn_readlane(d.rsrc, j);
-            rv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (M > 0 && act) rv[j] = ld4(xc + row * ld_x + lo);
-        }
-        // next item's descriptors load while this item's rows are in flight
-        CliqueDesc<G, RW> dn = d;
-        if (PERSIST && t + gridDim.x < n_items)
-            load_clique_desc<WAVES, RPW, G, RW>(dn, t + gridDim.x, n_cliques, p, wave, lane, clique_ptr,
-                                                member_row, member_group, coef, res_ptr, res_col, res_val);
+        load_res_desc<RPW, G, RW>(d, lane, res_col, res_val);
         // 2. group sums: per wave, then across waves through LDS
         float4 s[G];
 #pragma unroll
@@ -332,6 +327,51 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
+        // 3. own term and residual terms (gateway edges) in place, BEFORE any store: v[r] := a_r x_r
+        //    + sum_res w x_src.  On CDNA vmcnt counts stores too, so a gather issued after a store
+        //    would make the gather's wait drain that store from HBM first.  The wave's first RW
+        //    entries come lane-parallel and are gathered RU rows at a time (unconditional, clamped);
+        //    entries beyond RW (a wave with more than RW residual terms) take a per-entry loop.
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[0]), r));
+            v[r] = make_float4(af * v[r].x, af * v[r].y, af * v[r].z, af * v[r].w);
+        }
+        const int nres = d.nres;
+        const int npre = nres < RW ? nres : RW;
+        for (int j0 = 0; j0 < npre; j0 += RU) {
+            float4 xr[RU];
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int jj = j0 + u < npre ? j0 + u : npre - 1;
+                const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jj);
+                xr[u] = act ? ld4(xc + row * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                if (j0 + u >= npre) break;
+                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j0 + u));
+                const int slot = __builtin_amdgcn_readlane(d.rslot, j0 + u);
+#pragma unroll
+                for (int r = 0; r < RPW; ++r)
+                    if (slot == r) v[r] = axpy4<false>(w, xr[u], v[r]);
+            }
+        }
+        if (nres > RW) {
+            int pre = 0;
+            for (int r = 0; r < RPW && wave + WAVES * r < M; ++r) {
+                const int32_t m = d.m0 + wave + WAVES * r;
+                const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
+                for (int32_t q = rb + (RW > pre ? (RW - pre < re - rb ? RW - pre : re - rb) : 0); q < re; ++q) {
+                    const float4 xr = act ? ld4(xc + (int64_t)res_col[q] * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int rr = 0; rr < RPW; ++rr)
+                        if (rr == r) v[rr] = axpy4<false>(res_val[q], xr, v[rr]);
+                }
+                pre += re - rb;
+            }
+        }
+        // 4. group sums across waves through LDS
         __syncthreads();
         if (wave < G) {
             float4 a = red[wave][0][lane];
@@ -345,13 +385,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         __syncthreads();
 #pragma unroll
         for (int g = 0; g < G; ++g) s[g] = tot[g][lane];
-        // 3. outputs
-        int pre = 0;
+        // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here)
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
             if (wave + WAVES * r < M) {
-                const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[0]), r));
-                float4 o = make_float4(af * v[r].x, af * v[r].y, af * v[r].z, af * v[r].w);
+                float4 o = v[r];
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const float cg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[1 + g]), r));
@@ -360,33 +398,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                     o.z = __builtin_fmaf(cg, s[g].z, o.z);
                     o.w = __builtin_fmaf(cg, s[g].w, o.w);
                 }
-                const int32_t rb = __builtin_amdgcn_readlane(d.rb, r);
-                const int32_t re = __builtin_amdgcn_readlane(d.re, r);
                 const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-                if (rb < re) {
-                    // entries [pre, pre + re - rb) of this wave's residual list
-#pragma unroll
-                    for (int j = 0; j < RW; ++j)
-                        if (j >= pre && j < pre + (re - rb)) {
-                            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j));
-                            o = axpy4<false>(w, rv[j], o);
-                        }
-                    for (int32_t q = rb + (RW > pre ? RW - pre : 0); q < re; ++q) {   // beyond the prefetch
-                        const float4 xr = act ? ld4(xc + (int64_t)res_col[q] * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
-                        o = axpy4<false>(res_val[q], xr, o);
-                    }
-                    pre += re - rb;
-                }
                 if (act) st4_nt(yc + row * ld_y + lo, o);
             }
-        }
-        if (PERSIST) {
-            d = dn;
-            __syncthreads();   // tot[] / red[] are rewritten by the next item
-        } else if (t + gridDim.x < n_items) {
-            __syncthreads();
-            load_clique_desc<WAVES, RPW, G, RW>(d, t + gridDim.x, n_cliques, p, wave, lane, clique_ptr,
-                                                member_row, member_group, coef, res_ptr, res_col, res_val);
         }
     }
 }
@@ -858,22 +872,7 @@ bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) 
 template <int WAVES, int RPW, int G, int OCC, int RW, int FL>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
-    int64_t grid = grid_for(n_items);
-    if (FL & 1) {
-        // one resident wave of blocks, each walking items t, t+grid, ... (grid % 8 == 0 keeps the
-        // XCD mapping); residency from the occupancy query, cached per instantiation
-        static int blocks_per_cu = 0, n_cu = 0;
-        if (!blocks_per_cu) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &blocks_per_cu, k_mix_clique<WAVES, RPW, G, OCC, RW, FL>, WAVES * 64, 0);
-            if (blocks_per_cu < 1) blocks_per_cu = 1;
-        }
-        const int64_t resident = ((int64_t)blocks_per_cu * n_cu + 7) / 8 * 8;
-        if (resident < grid) grid = resident;
-    }
+    const int64_t grid = n_items;   // one block per (clique, chunk) item; < 2^31 checked by the caller
     hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
@@ -894,18 +893,16 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 }
 
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
-// targets, RW = residual rows prefetched per wave, FL = flags (1 persistent grid, 2 nt loads).
-// NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<onebar> overrides the choice (tuning only).
+// targets, RW = residual entries per wave held lane-parallel (gathered in batches; more fall back
+// to a per-entry loop), FL = flags (2: non-temporal member loads).
+// NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                         const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0;
     if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob);
     const int mc = pl->max_clique;
     if (waves * rpw < mc) {
-        // measured (tools/tune_inproc.py, 1000-node d-cliques, P=2^20): 16x7 and 8x13 within 1%
-        // of each other and within 2-7% of a plain copy with the same access pattern; residual
-        // prefetch (rw) and persistent grids did not pay.
-        rw = 0; ob = 0;
+        rw = 64; ob = 0;
         if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
         else if (mc <= 32) { waves = 8; rpw = 4; occ = 8; }
         else if (mc <= 64) { waves = 16; rpw = 4; occ = 8; }
@@ -915,12 +912,11 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
     }
 #define NIIDMIX_TILE(W, R, O, RWV, OB) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB) return launch_clique_g<W, R, O, RWV, OB>(x, ld_x, y, ld_y, p, pl, n_items, s)
-    NIIDMIX_TILE(8, 2, 8, 0, 0); NIIDMIX_TILE(8, 4, 8, 0, 0); NIIDMIX_TILE(16, 4, 8, 0, 0);
-    NIIDMIX_TILE(16, 7, 8, 0, 0); NIIDMIX_TILE(16, 8, 4, 0, 0); NIIDMIX_TILE(16, 16, 4, 0, 0);
-    // tuning alternatives (NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>, flags: 1 =
-    // persistent grid, 2 = non-temporal member loads)
-    NIIDMIX_TILE(8, 13, 4, 0, 0); NIIDMIX_TILE(8, 13, 4, 2, 0); NIIDMIX_TILE(8, 13, 4, 2, 1);
-    NIIDMIX_TILE(16, 7, 8, 2, 0); NIIDMIX_TILE(16, 7, 8, 0, 2); NIIDMIX_TILE(8, 13, 4, 0, 2);
+    NIIDMIX_TILE(8, 2, 8, 64, 0); NIIDMIX_TILE(8, 4, 8, 64, 0); NIIDMIX_TILE(16, 4, 8, 64, 0);
+    NIIDMIX_TILE(16, 7, 8, 64, 0); NIIDMIX_TILE(16, 8, 4, 64, 0); NIIDMIX_TILE(16, 16, 4, 64, 0);
+    // tuning alternatives
+    NIIDMIX_TILE(16, 7, 8, 0, 0); NIIDMIX_TILE(16, 7, 8, 64, 2); NIIDMIX_TILE(8, 13, 4, 64, 0);
+    NIIDMIX_TILE(8, 13, 4, 64, 2);
 #undef NIIDMIX_TILE
     return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%d", waves, rpw, occ, rw, ob);
 }
@@ -1005,6 +1001,7 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     const int64_t n_items = (int64_t)plan->n_cliques * ((n_chunks + 7) / 8) * 8;
     if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))
         return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique, chunk) items for one grid");
     return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, n_items, s);
 }
 

@@ -27,11 +27,15 @@ def main():
     ap.add_argument("--config", default="dcliques1000")
     ap.add_argument("--variants", default="16x7x8x0x0,16x7x8x0x2")
     ap.add_argument("--ld-pad", type=int, default=0)
+    ap.add_argument("--no-res", action="store_true",
+                    help="timing experiment only (WRONG results): drop the residual terms")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     csr, cliques, p, _ = bench.single_gpu_topology(a.config)
     m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
     n = csr.n
+    if a.no_res:
+        m.p_res_ptr.zero_()
     ld = p + a.ld_pad
     x = torch.randn(n, ld, device=dev)[:, :p]
     y = torch.empty(n, ld, device=dev)[:, :p]
