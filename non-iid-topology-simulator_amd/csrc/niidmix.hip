@@ -778,27 +778,29 @@ __global__ __launch_bounds__(256) void k_mix_tile(
                 }
             }
         }
-        // update_models: z + acc with z = x_self*0 (the self row is re-read: L2-resident, every
-        // position load of the tile's clique touched it) — saves RT*NE registers
+        // update_models: z + acc with z = x_self*0 (the self rows are re-read: L2-resident, every
+        // position load of the tile's clique touched them) — all RT re-reads are issued before the
+        // first store, into the registers the position loads used, so the stores go out back to
+        // back (vmcnt counts stores too on CDNA: a load between two stores would drain the first)
+        if (!avg_only) {
+#pragma unroll
+            for (int r = 0; r < RT; ++r) {
+                const int row = __builtin_amdgcn_readlane(d_row, r);
+                float xs[NE];
+#pragma unroll
+                for (int q = 0; q < S; ++q) ldv<VW>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cs[q], xs + q * VW);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) acc[r][e] = xs[e] * 0.f + acc[r][e];
+            }
+        }
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
             const int row = __builtin_amdgcn_readlane(d_row, r);
             if (row < 0) continue;                                  // wave-uniform
-            float o[NE];
-            if (avg_only) {
-#pragma unroll
-                for (int e = 0; e < NE; ++e) o[e] = acc[r][e];
-            } else {
-                float xs[NE];
-#pragma unroll
-                for (int q = 0; q < S; ++q) ldv<VW>(x + (int64_t)row * ld_x + cs[q], xs + q * VW);
-#pragma unroll
-                for (int e = 0; e < NE; ++e) o[e] = xs[e] * 0.f + acc[r][e];
-            }
             float *dst = y + (int64_t)row * ld_y;
 #pragma unroll
             for (int q = 0; q < S; ++q)
-                if (ok[q]) stv_nt<VW>(dst + cs[q], o + q * VW);
+                if (ok[q]) stv_nt<VW>(dst + cs[q], acc[r] + q * VW);
         }
     }
 }

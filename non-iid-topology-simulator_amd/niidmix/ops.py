@@ -247,11 +247,12 @@ class Mixer:
             self.s_src_ptr = torch.from_numpy(sp.src_ptr).to(dev)
             self.s_src_rows = torch.from_numpy(sp.src_rows).to(dev)
             self.s_scol = torch.from_numpy(sp.scol).to(dev)
-        # merged-order row tiles (exact mode's fast path): only worth building when rows read many
-        # sources (avg degree >= 8); NIIDMIX_TILE_RT=8|16|32 picks the tile height
+        # merged-order row tiles (exact mode's default kernel): only worth building when rows read
+        # many sources (avg degree >= 8); NIIDMIX_TILE_RT=8|16|32 picks the tile height (8 measured
+        # fastest: 5.9 ms vs 6.7 / 8.5 ms for 16 / 32 on the 1000-node d-cliques round)
         self.tile, self.tile_reason = (None, "average degree < 8")
         if csr.nnz >= 9 * max(csr.n, 1):
-            rt = int(os.environ.get("NIIDMIX_TILE_RT", "16"))
+            rt = int(os.environ.get("NIIDMIX_TILE_RT", "8"))
             self.tile, self.tile_reason = build_tile_plan(csr, cliques, rt)
         if self.tile is not None:
             tp = self.tile
@@ -267,9 +268,10 @@ class Mixer:
 
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
-            # the LDS-staged exact kernel measured no faster than the L2-served CSR gather on the
-            # 1000-node d-cliques round (23.8 vs 23.8 ms) and slower on ring-100: CSR by default
-            return "csr-exact"
+            # measured on the 1000-node d-cliques round (P = 2^20): merged-order row tiles of 8
+            # rows 5.9 ms, CSR gather 23.1 ms, LDS-staged 23.9 ms; the tile plan exists only for
+            # graphs with average degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
+            return "tile-exact" if self.tile is not None else "csr-exact"
         if self.plan is not None and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:

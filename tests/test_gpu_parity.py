@@ -100,7 +100,7 @@ def test_auto_kernel_choice(gpu):
     g = load_golden("dcliques1000_fc_p64")
     m = _mixer(g, gpu)
     assert m.kernel_for("fast") == "clique"
-    assert m.kernel_for("exact") == "csr-exact"
+    assert m.kernel_for("exact") == "tile-exact"
     g = load_golden("fc64_p33")
     assert _mixer(g, gpu).kernel_for("fast") == "clique"      # MH fully-connected = one clique
     ops = _ops()
@@ -115,6 +115,7 @@ def test_auto_kernel_choice(gpu):
     assert ops.Mixer(csr=csr, device=gpu).kernel_for("fast") == "dense"
     g = load_golden("ring100_p257")
     assert _mixer(g, gpu).kernel_for("fast") == "csr-fast"
+    assert _mixer(g, gpu).kernel_for("exact") == "csr-exact"   # degree 2: no tile plan
 
 
 def _dcliques_full(gpu, p, seed=0):
