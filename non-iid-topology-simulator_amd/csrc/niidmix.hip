@@ -71,13 +71,6 @@ __device__ __forceinline__ float4 ld4_nt(const float *p) {
     return make_float4(v[0], v[1], v[2], v[3]);
 }
 
-__device__ __forceinline__ void st4_nt(float *p, float4 v) {
-    __builtin_nontemporal_store(v.x, p + 0);
-    __builtin_nontemporal_store(v.y, p + 1);
-    __builtin_nontemporal_store(v.z, p + 2);
-    __builtin_nontemporal_store(v.w, p + 3);
-}
-
 // ----------------------------------------------------------------------------------------------
 // Exact / fast per-element update rules.
 //   exact: acc = fl(acc + fl(w*x))      (ATen CPU add_(w*p): separate roundings, no FMA)
@@ -218,7 +211,7 @@ struct CliqueDesc {        // one work item's member descriptors, lane-parallel 
     float rw;              //   weight)
 };
 
-template <int WAVES, int RPW, int G, int RW>
+template <int WAVES, int RPW, int G, int RW, int64_t CW>
 __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t, int32_t n_cliques,
                                                  int64_t p, int wave, int lane,
                                                  const int32_t *__restrict__ clique_ptr,
@@ -230,7 +223,7 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
     const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
     const int32_t cq = (int32_t)(local % n_cliques);
     d.m0 = clique_ptr[cq];
-    d.M = chunk * kChunk < p ? clique_ptr[cq + 1] - d.m0 : 0;
+    d.M = chunk * CW < p ? clique_ptr[cq + 1] - d.m0 : 0;
     const int kd = wave + WAVES * lane;
     d.row = 0; d.grp = 0; d.rb = 0; d.re = 0;
 #pragma unroll
@@ -271,7 +264,15 @@ __device__ __forceinline__ void load_res_desc(CliqueDesc<G, RW> &d, int lane,
     }
 }
 
-template <int WAVES, int RPW, int G, int OCC, int RW, int FL>
+template <int V> __device__ __forceinline__ void ldv_nt(const float *p, float *o);
+template <> __device__ __forceinline__ void ldv_nt<4>(const float *p, float *o) {
+    const float4 v = ld4_nt(p); o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+
+// V = columns per lane per row: 4 (float4, 256-column chunks; cliques up to WAVES*RPW <= 256) or 1
+// (one float, 64-column chunks; not instantiated yet: with RPW up to 64 rows per wave the
+// compiler hoists every row address into scalar registers and spills).
+template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
@@ -279,41 +280,49 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
+    static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
     constexpr int RU = 2;                     // residual rows gathered per batch
-    __shared__ float4 red[G][WAVES][kWave];
-    __shared__ float4 tot[G][kWave];
+    constexpr int64_t CW = 64 * V;            // columns per work item
+    __shared__ float red[G][WAVES][kWave * V];
+    __shared__ float tot[G][kWave * V];
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
-    {
-        const int64_t t = blockIdx.x;             // one work item per block (grid = n_items)
-        if (t >= n_items) return;
-        CliqueDesc<G, RW> d;
-        load_clique_desc<WAVES, RPW, G, RW>(d, t, n_cliques, p, wave, lane, clique_ptr, member_row,
+    const int64_t t = blockIdx.x;             // one work item per block (grid = n_items)
+    if (t >= n_items) return;
+    CliqueDesc<G, RW> d;
+    load_clique_desc<WAVES, RPW, G, RW, CW>(d, t, n_cliques, p, wave, lane, clique_ptr, member_row,
                                             member_group, coef, res_ptr);
-        const int64_t local = t >> 3;
-        const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
-        const bool act = chunk * kChunk + 4 * lane < p;
-        const int32_t M = d.M;
-        const float *xc = x + chunk * kChunk;
-        float *yc = y + chunk * kChunk;
-        const unsigned lo = 4u * (unsigned)lane;
+    const int64_t local = t >> 3;
+    const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
+    const bool act = chunk * CW + V * lane < p;
+    const int32_t M = d.M;
+    const float *xc = x + chunk * CW;
+    float *yc = y + chunk * CW;
+    const unsigned lo = (unsigned)(V * lane);
 
-        // 1. member rows -> registers, all loads in flight before the first use
-        float4 v[RPW];
+    // 1. member rows -> registers, all loads in flight before the first use
+    float v[RPW][V];
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (wave + WAVES * r < M) {
-                const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-                if (act) v[r] = NTL ? ld4_nt(xc + row * ld_x + lo) : ld4(xc + row * ld_x + lo);
+    for (int r = 0; r < RPW; ++r) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[r][e] = 0.f;
+        if (wave + WAVES * r < M) {
+            const int64_t row = __builtin_amdgcn_readlane(d.row, r);
+            if (act) {
+                if (NTL) ldv_nt<V>(xc + row * ld_x + lo, v[r]);
+                else ldv<V>(xc + row * ld_x + lo, v[r]);
             }
         }
-        load_res_desc<RPW, G, RW>(d, lane, res_col, res_val);
-        // 2. group sums: per wave, then across waves through LDS
-        float4 s[G];
+    }
+    load_res_desc<RPW, G, RW>(d, lane, res_col, res_val);
+    // 2. per-wave partial group sums -> LDS
+    {
+        float s[G][V];
 #pragma unroll
-        for (int g = 0; g < G; ++g) s[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int e = 0; e < V; ++e) s[g][e] = 0.f;
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
             if (wave + WAVES * r < M) {
@@ -321,86 +330,105 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     if (gr == g) {
-                        s[g].x += v[r].x; s[g].y += v[r].y; s[g].z += v[r].z; s[g].w += v[r].w;
+#pragma unroll
+                        for (int e = 0; e < V; ++e) s[g][e] += v[r][e];
                     }
             }
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
-        // 3. own term and residual terms (gateway edges) in place, BEFORE any store: v[r] := a_r x_r
-        //    + sum_res w x_src.  On CDNA vmcnt counts stores too, so a gather issued after a store
-        //    would make the gather's wait drain that store from HBM first.  The wave's first RW
-        //    entries come lane-parallel and are gathered RU rows at a time (unconditional, clamped);
-        //    entries beyond RW (a wave with more than RW residual terms) take a per-entry loop.
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[0]), r));
-            v[r] = make_float4(af * v[r].x, af * v[r].y, af * v[r].z, af * v[r].w);
+        for (int g = 0; g < G; ++g) {
+            if (V == 4) *reinterpret_cast<float4 *>(&red[g][wave][4 * lane]) = make_float4(s[g][0], s[g][V > 1 ? 1 : 0], s[g][V > 2 ? 2 : 0], s[g][V > 3 ? 3 : 0]);
+            else red[g][wave][lane] = s[g][0];
         }
-        const int nres = d.nres;
-        const int npre = nres < RW ? nres : RW;
-        for (int j0 = 0; j0 < npre; j0 += RU) {
-            float4 xr[RU];
+    }
+    // 3. own term and residual terms (gateway edges) in place, BEFORE any store: v[r] := a_r x_r
+    //    + sum_res w x_src.  On CDNA vmcnt counts stores too, so a gather issued after a store
+    //    would make the gather's wait drain that store from HBM first.  The wave's first RW
+    //    entries come lane-parallel and are gathered RU rows at a time (unconditional, clamped);
+    //    entries beyond RW (a wave with more than RW residual terms) take a per-entry loop.
 #pragma unroll
-            for (int u = 0; u < RU; ++u) {
-                const int jj = j0 + u < npre ? j0 + u : npre - 1;
-                const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jj);
-                xr[u] = act ? ld4(xc + row * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+    for (int r = 0; r < RPW; ++r) {
+        const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[0]), r));
 #pragma unroll
-            for (int u = 0; u < RU; ++u) {
-                if (j0 + u >= npre) break;
-                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j0 + u));
-                const int slot = __builtin_amdgcn_readlane(d.rslot, j0 + u);
+        for (int e = 0; e < V; ++e) v[r][e] *= af;
+    }
+    const int nres = d.nres;
+    const int npre = nres < RW ? nres : RW;
+    for (int j0 = 0; j0 < npre; j0 += RU) {
+        float xr[RU][V];
 #pragma unroll
-                for (int r = 0; r < RPW; ++r)
-                    if (slot == r) v[r] = axpy4<false>(w, xr[u], v[r]);
-            }
+        for (int u = 0; u < RU; ++u) {
+            const int jj = j0 + u < npre ? j0 + u : npre - 1;
+            const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jj);
+#pragma unroll
+            for (int e = 0; e < V; ++e) xr[u][e] = 0.f;
+            if (act) ldv<V>(xc + row * ld_x + lo, xr[u]);
         }
-        if (nres > RW) {
-            int pre = 0;
-            for (int r = 0; r < RPW && wave + WAVES * r < M; ++r) {
-                const int32_t m = d.m0 + wave + WAVES * r;
-                const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
-                for (int32_t q = rb + (RW > pre ? (RW - pre < re - rb ? RW - pre : re - rb) : 0); q < re; ++q) {
-                    const float4 xr = act ? ld4(xc + (int64_t)res_col[q] * ld_x + lo) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                    for (int rr = 0; rr < RPW; ++rr)
-                        if (rr == r) v[rr] = axpy4<false>(res_val[q], xr, v[rr]);
+        for (int u = 0; u < RU; ++u) {
+            if (j0 + u >= npre) break;
+            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j0 + u));
+            const int slot = __builtin_amdgcn_readlane(d.rslot, j0 + u);
+#pragma unroll
+            for (int r = 0; r < RPW; ++r)
+                if (slot == r) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xr[u][e], v[r][e]);
                 }
-                pre += re - rb;
-            }
         }
-        // 4. group sums across waves through LDS
-        __syncthreads();
-        if (wave < G) {
-            float4 a = red[wave][0][lane];
+    }
+    if (nres > RW) {
+        int pre = 0;
+        for (int r = 0; r < RPW && wave + WAVES * r < M; ++r) {
+            const int32_t m = d.m0 + wave + WAVES * r;
+            const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
+            for (int32_t q = rb + (RW > pre ? (RW - pre < re - rb ? RW - pre : re - rb) : 0); q < re; ++q) {
+                float xr[V];
+#pragma unroll
+                for (int e = 0; e < V; ++e) xr[e] = 0.f;
+                if (act) ldv<V>(xc + (int64_t)res_col[q] * ld_x + lo, xr);
+                const float w = res_val[q];
+#pragma unroll
+                for (int rr = 0; rr < RPW; ++rr)
+                    if (rr == r) {
+#pragma unroll
+                        for (int e = 0; e < V; ++e) v[rr][e] = __builtin_fmaf(w, xr[e], v[rr][e]);
+                    }
+            }
+            pre += re - rb;
+        }
+    }
+    // 4. group sums across waves through LDS (waves 0..G-1 each reduce one group)
+    __syncthreads();
+    if (wave < G) {
+        float a[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) a[e] = red[wave][0][V * lane + e];
 #pragma unroll 4
-            for (int w = 1; w < WAVES; ++w) {
-                const float4 b = red[wave][w][lane];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        for (int w = 1; w < WAVES; ++w)
+#pragma unroll
+            for (int e = 0; e < V; ++e) a[e] += red[wave][w][V * lane + e];
+#pragma unroll
+        for (int e = 0; e < V; ++e) tot[wave][V * lane + e] = a[e];
+    }
+    __syncthreads();
+    float sg[G][V];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < V; ++e) sg[g][e] = tot[g][V * lane + e];
+    // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        if (wave + WAVES * r < M) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float cg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[1 + g]), r));
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(cg, sg[g][e], v[r][e]);
             }
-            tot[wave][lane] = a;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int g = 0; g < G; ++g) s[g] = tot[g][lane];
-        // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here)
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            if (wave + WAVES * r < M) {
-                float4 o = v[r];
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const float cg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[1 + g]), r));
-                    o.x = __builtin_fmaf(cg, s[g].x, o.x);
-                    o.y = __builtin_fmaf(cg, s[g].y, o.y);
-                    o.z = __builtin_fmaf(cg, s[g].z, o.z);
-                    o.w = __builtin_fmaf(cg, s[g].w, o.w);
-                }
-                const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-                if (act) st4_nt(yc + row * ld_y + lo, o);
-            }
+            const int64_t row = __builtin_amdgcn_readlane(d.row, r);
+            if (act) stv_nt<V>(yc + row * ld_y + lo, v[r]);
         }
     }
 }
@@ -701,7 +729,7 @@ __global__ __launch_bounds__(256) void k_mix_tile(
     int64_t n_sub_groups, int64_t n_items, int avg_only) {
     constexpr int S = NE / VW;                  // slots per lane
     constexpr int64_t CW = 64 * NE;             // columns per work item
-    constexpr uint32_t FULL = RT == 32 ? 0xffffffffu : ((1u << RT) - 1u);
+    constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                        // positions whose loads are in flight together
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
@@ -871,24 +899,27 @@ bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) 
     return a < b + b_elems && b < a + a_elems;
 }
 
-template <int WAVES, int RPW, int G, int OCC, int RW, int FL>
+template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
     const int64_t grid = n_items;   // one block per (clique, chunk) item; < 2^31 checked by the caller
-    hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL, V>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
                        pl->res_val, n_items);
 }
 
-template <int WAVES, int RPW, int OCC, int RW, int FL>
+template <int WAVES, int RPW, int OCC, int RW, int FL, int V>
 int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
+                    const niidmix_clique_plan *pl, hipStream_t s) {
+    const int64_t n_chunks = (p + 64 * V - 1) / (64 * V);
+    const int64_t n_items = (int64_t)pl->n_cliques * ((n_chunks + 7) / 8) * 8;
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique, chunk) items for one grid");
     switch (pl->n_groups) {
-        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, FL>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
     return check_launch("k_mix_clique");
@@ -896,15 +927,18 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
 // targets, RW = residual entries per wave held lane-parallel (gathered in batches; more fall back
-// to a per-entry loop), FL = flags (2: non-temporal member loads).
-// NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags> overrides the choice (tuning only).
+// to a per-entry loop), FL = flags (2: non-temporal member loads), V = columns per lane (4 when the
+// slab allows float4 access and the clique fits 256 rows, else 1).
+// NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>x<v> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                        const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
-    int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0;
-    if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob);
+                        const niidmix_clique_plan *pl, bool vec4, hipStream_t s) {
+    int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0, v = 0;
+    if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob, &v);
+    if (v == 0) v = 4;
     const int mc = pl->max_clique;
+    if (!vec4) return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
     if (waves * rpw < mc) {
-        rw = 64; ob = 0;
+        rw = 64; ob = 0; v = 4;
         if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
         else if (mc <= 32) { waves = 8; rpw = 4; occ = 8; }
         else if (mc <= 64) { waves = 16; rpw = 4; occ = 8; }
@@ -913,14 +947,13 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         else if (mc <= 256) { waves = 16; rpw = 16; occ = 4; }
         else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
     }
-#define NIIDMIX_TILE(W, R, O, RWV, OB) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB) return launch_clique_g<W, R, O, RWV, OB>(x, ld_x, y, ld_y, p, pl, n_items, s)
-    NIIDMIX_TILE(8, 2, 8, 64, 0); NIIDMIX_TILE(8, 4, 8, 64, 0); NIIDMIX_TILE(16, 4, 8, 64, 0);
-    NIIDMIX_TILE(16, 7, 8, 64, 0); NIIDMIX_TILE(16, 8, 4, 64, 0); NIIDMIX_TILE(16, 16, 4, 64, 0);
+#define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s)
+    NIIDMIX_TILE(8, 2, 8, 64, 0, 4); NIIDMIX_TILE(8, 4, 8, 64, 0, 4); NIIDMIX_TILE(16, 4, 8, 64, 0, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 8, 4, 64, 0, 4); NIIDMIX_TILE(16, 16, 4, 64, 0, 4);
     // tuning alternatives
-    NIIDMIX_TILE(16, 7, 8, 0, 0); NIIDMIX_TILE(16, 7, 8, 64, 2); NIIDMIX_TILE(8, 13, 4, 64, 0);
-    NIIDMIX_TILE(8, 13, 4, 64, 2);
+    NIIDMIX_TILE(16, 7, 8, 0, 0, 4); NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 0, 4);
 #undef NIIDMIX_TILE
-    return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%d", waves, rpw, occ, rw, ob);
+    return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%dx%d", waves, rpw, occ, rw, ob, v);
 }
 
 }  // namespace
@@ -984,7 +1017,9 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (plan->max_clique > 256) {                     // big cliques: two-pass, one lane per column
+    const bool vec4 = (p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y);
+    if (plan->max_clique > 256) {
+        // big cliques (e.g. fully-connected = one clique): two-pass, one lane per column
         const int64_t n_ch = (p + kWave - 1) / kWave;
         const int64_t items = (int64_t)plan->n_cliques * ((n_ch + 7) / 8) * 8;
         const dim3 grid((unsigned)grid_for(items)), block(256);
@@ -999,12 +1034,7 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
 #undef NIIDMIX_BIG
         return check_launch("k_mix_bigclique");
     }
-    const int64_t n_chunks = (p + kChunk - 1) / kChunk;
-    const int64_t n_items = (int64_t)plan->n_cliques * ((n_chunks + 7) / 8) * 8;
-    if (!((p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y)))
-        return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
-    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique, chunk) items for one grid");
-    return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, n_items, s);
+    return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, vec4, s);
 }
 
 int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
