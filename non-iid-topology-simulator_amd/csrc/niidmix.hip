@@ -542,21 +542,22 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
 
 // ----------------------------------------------------------------------------------------------
 // Clique-factored mixing for BIG cliques (> 256 members, e.g. a fully-connected topology with MH
-// weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), 4 waves, lane = one
-// column.  Pass 1 streams the members (wave w: a contiguous quarter) into per-group sums, an LDS
-// reduction combines the waves; pass 2 streams the members again and writes
+// weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), WAVES waves, lane =
+// one column.  Pass 1 streams the members (wave w: a contiguous 1/WAVES of them) into per-group
+// sums, an LDS reduction combines the waves; pass 2 streams the members again and writes
 // y = a x + sum_g c_g S_g (+ residual terms).  The pass-2 re-read (M x 256 B per item) is served
-// from L2 / the 256 MiB Infinity Cache, so HBM sees ~1 read + 1 write per parameter: an
-// HBM-bound alternative to the MFMA GEMM for dense-but-structured W.
-template <int G>
-__global__ __launch_bounds__(256) void k_mix_bigclique(
+// by L2 / the Infinity Cache for the most part.  Pass 2 is software-pipelined: the next U rows
+// are loaded before this batch's U stores, because vmcnt counts stores too on CDNA (a load issued
+// after a store would make its wait drain the store).
+template <int G, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
     constexpr int U = 8;
-    __shared__ float red[G][4][kWave];
+    __shared__ float red[G][WAVES][kWave];
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
     for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
@@ -572,8 +573,8 @@ __global__ __launch_bounds__(256) void k_mix_bigclique(
         float *yc = y + c0;
         const int32_t m0 = clique_ptr[cq];
         const int32_t M = clique_ptr[cq + 1] - m0;
-        const int32_t per = (M + 3) / 4;
-        const int32_t kb = m0 + wave * per;
+        const int32_t per = (M + WAVES - 1) / WAVES;
+        const int32_t kb = m0 + (wave * per < M ? wave * per : M);
         const int32_t ke = m0 + ((wave + 1) * per < M ? (wave + 1) * per : M);
         float s[G];
 #pragma unroll
@@ -595,25 +596,42 @@ __global__ __launch_bounds__(256) void k_mix_bigclique(
         for (int g = 0; g < G; ++g) red[g][wave][lane] = s[g];
         __syncthreads();
 #pragma unroll
-        for (int g = 0; g < G; ++g) s[g] = (red[g][0][lane] + red[g][1][lane]) + (red[g][2][lane] + red[g][3][lane]);
+        for (int g = 0; g < G; ++g) {
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) a += red[g][w][lane];
+            s[g] = a;
+        }
         __syncthreads();                                      // red[] is rewritten by the next item
-        for (int32_t k = kb; k < ke; k += U) {
+        if (kb < ke) {
             float v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                v[u] = xc[(int64_t)member_row[k + u < ke ? k + u : kb] * ld_x + lo];
+                v[u] = xc[(int64_t)member_row[kb + u < ke ? kb + u : kb] * ld_x + lo];
+            for (int32_t k = kb; k < ke; k += U) {
+                // own terms and residual gathers of this batch (loads, before any store of it)
+                float o[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (k + u < ke) {
-                    const int32_t m = k + u;
+                for (int u = 0; u < U; ++u) {
+                    const int32_t m = k + u < ke ? k + u : kb;
                     const float *cf = coef + (int64_t)m * (1 + G);
-                    float o = cf[0] * v[u];
+                    o[u] = cf[0] * v[u];
 #pragma unroll
-                    for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g], o);
-                    for (int32_t q = res_ptr[m]; q < res_ptr[m + 1]; ++q)
-                        o = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x + lo], o);
-                    if (act) __builtin_nontemporal_store(o, yc + (int64_t)member_row[m] * ld_y + lane);
+                    for (int g = 0; g < G; ++g) o[u] = __builtin_fmaf(cf[1 + g], s[g], o[u]);
+                    if (k + u < ke)
+                        for (int32_t q = res_ptr[m]; q < res_ptr[m + 1]; ++q)
+                            o[u] = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x + lo], o[u]);
                 }
+                // next batch's rows in flight before this batch's stores
+                const int32_t kn = k + U;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    v[u] = kn < ke ? xc[(int64_t)member_row[kn + u < ke ? kn + u : kn] * ld_x + lo] : 0.f;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (k + u < ke && act)
+                        __builtin_nontemporal_store(o[u], yc + (int64_t)member_row[k + u] * ld_y + lane);
+            }
         }
     }
 }
@@ -1019,18 +1037,32 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool vec4 = (p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y);
     if (plan->max_clique > 256) {
-        // big cliques (e.g. fully-connected = one clique): two-pass, one lane per column
+        // big cliques (e.g. fully-connected = one clique): two-pass, one lane per column, a grid of
+        // bpc blocks per CU walking the items.  Measured on FC-1000, P = 2^20 (tools/ab_clique.py):
+        // 8 waves x 16 blocks/CU 2.36 ms; capping residency (to keep the pass-2 re-read in the
+        // Infinity Cache) was slower: 8x4 2.57, 16x1 2.95 ms.  NIIDMIX_BIG=<waves>x<blocks per CU>
+        // overrides (tuning).
+        int waves = 8, bpc = 16;
+        if (const char *e = getenv("NIIDMIX_BIG")) sscanf(e, "%dx%d", &waves, &bpc);
+        if (bpc < 1) bpc = 1;
+        static int n_cu = 0;
+        if (!n_cu) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
+        }
         const int64_t n_ch = (p + kWave - 1) / kWave;
         const int64_t items = (int64_t)plan->n_cliques * ((n_ch + 7) / 8) * 8;
-        const dim3 grid((unsigned)grid_for(items)), block(256);
-#define NIIDMIX_BIG(G) hipLaunchKernelGGL((k_mix_bigclique<G>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, items)
-        switch (plan->n_groups) {
-            case 1: NIIDMIX_BIG(1); break;
-            case 2: NIIDMIX_BIG(2); break;
-            case 3: NIIDMIX_BIG(3); break;
-            case 4: NIIDMIX_BIG(4); break;
-            default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
-        }
+        int64_t gsz = ((int64_t)bpc * n_cu + 7) / 8 * 8;
+        if (gsz > items) gsz = items;
+        const dim3 grid((unsigned)gsz), block(waves * 64);
+        const size_t lds = 0;
+#define NIIDMIX_BIG(G, W) hipLaunchKernelGGL((k_mix_bigclique<G, W>), grid, block, lds, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, items)
+#define NIIDMIX_BIGW(W) switch (plan->n_groups) { case 1: NIIDMIX_BIG(1, W); break; case 2: NIIDMIX_BIG(2, W); break; case 3: NIIDMIX_BIG(3, W); break; case 4: NIIDMIX_BIG(4, W); break; default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups); }
+        if (waves == 4) { NIIDMIX_BIGW(4); }
+        else if (waves == 8) { NIIDMIX_BIGW(8); }
+        else { NIIDMIX_BIGW(16); }
+#undef NIIDMIX_BIGW
 #undef NIIDMIX_BIG
         return check_launch("k_mix_bigclique");
     }

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--config", default="dcliques1000")
     ap.add_argument("--variants", default="16x7x8x0x0,16x7x8x0x2")
     ap.add_argument("--ld-pad", type=int, default=0)
+    ap.add_argument("--env", default="NIIDMIX_CLIQUE_TILE",
+                    help="environment variable the variants are assigned to (NIIDMIX_BIG for the "
+                         "big-clique kernel)")
     ap.add_argument("--no-res", action="store_true",
                     help="timing experiment only (WRONG results): drop the residual terms")
     a = ap.parse_args()
@@ -44,7 +47,7 @@ def main():
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.reps):
         for v in variants:
-            os.environ["NIIDMIX_CLIQUE_TILE"] = v
+            os.environ[a.env] = v
             for _ in range(3):
                 m(x, out=y, kernel="clique")
             torch.cuda.synchronize()
