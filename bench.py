@@ -42,6 +42,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "param-GB/s mixed (device-resident), 1000-node d-cliques, P=1M fp32"
+GRAD_METRIC = "gradient-GB/s averaged (device-resident), 1000-node d-cliques --clique-gradient, P=1M fp32"
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3
 
@@ -72,6 +73,10 @@ def parse():
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
     ap.add_argument("--ld-pad", type=int, default=0,
                     help="single GPU: pad every slab row by this many floats (ld = P + pad)")
+    ap.add_argument("--workload", default="mix", choices=["mix", "grad-clique"],
+                    help="mix: the headline neighbour mixing round; grad-clique: the --clique-gradient "
+                         "gradient mean (k_grad_segment_mean) over the same 1000-node d-cliques "
+                         "topology (single GPU)")
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
     return ap.parse_args()
@@ -205,6 +210,37 @@ def cpu_baseline(csr, p, sample_nodes):
                       f"{torch.get_num_threads()} threads: {t:.2f} s"}
 
 
+def cpu_baseline_grad(cliques, n, p):
+    """The reference's clique-gradient loop restated (oracle.reference_loop_clique_gradient), timed
+    on this host over the first clique (a bounded sample; every clique costs the same)."""
+    from oracle import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1)
+    clique = cliques[0]
+    nodes = {}
+    for r in clique:
+        m = torch.nn.Module()
+        m.w = torch.nn.Parameter(torch.zeros(p))
+        m.w.grad = torch.randn(p, generator=g)
+        nodes[r] = {"rank": r, "model": m}
+    reps = 0
+    t0 = time.perf_counter()
+    while True:                       # repeat the clique until ~5 s of CPU work (a single clique
+        oracle.reference_loop_clique_gradient(nodes, [clique])  # takes only ~10 ms at P = 2^20)
+        reps += 1
+        if time.perf_counter() - t0 > 5.0:
+            break
+    t = (time.perf_counter() - t0) / reps
+    k = len(clique)
+    return {"value": k * p * 4 / t / 1e9, "unit": "GB/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"the reference clique-gradient loop (oracle.reference_loop_clique_gradient) "
+                      f"over clique 0 ({k} of {n} nodes) at P={p}, torch {torch.__version__} CPU, "
+                      f"{torch.get_num_threads()} threads: {t * 1e3:.1f} ms per clique "
+                      f"(mean of {reps} repetitions)"}
+
+
 def _reference_partial(oracle, nodes, todo, topo):
     import copy
     W, edges = topo["weights"], topo["edges"]
@@ -242,10 +278,22 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from niidmix import ops
+    if args.workload != "mix" and world > 1:
+        raise SystemExit("--workload grad-clique is single-GPU")
     if world == 1:
         csr, cliques, p_default, desc = single_gpu_topology(args.config)
         p = args.p or p_default
-        mixer = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+        if args.workload == "grad-clique":
+            from niidmix.gradient import GradMean, build_grad_plan
+            if not cliques:
+                raise SystemExit(f"--workload grad-clique needs a clique topology, not {args.config}")
+            plan = build_grad_plan(csr.n, {"cliques": cliques, "edges": csr.edges()},
+                                   {"algorithm": {"clique-gradient": True}})
+            mixer = GradMean(plan, dev)
+            mixer.kernel_for = lambda mode, x=None: "grad-segment-mean"
+            desc = "clique gradient mean (--clique-gradient, d_sgd.py:56-65) over " + desc
+        else:
+            mixer = ops.Mixer(csr=csr, cliques=cliques, device=dev)
         n_local = n_total = csr.n
         parallelism = "single GPU"
         gen = torch.Generator(device=dev).manual_seed(args.seed)
@@ -348,9 +396,12 @@ def main():
             e2e = e2e_rounds(mixer, n_local, p, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(csr, p, args.cpu_sample_nodes)
+            if args.workload == "grad-clique":
+                cpu = cpu_baseline_grad(cliques, csr.n, p)
+            else:
+                cpu = cpu_baseline(csr, p, args.cpu_sample_nodes)
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+            "metric": METRIC if args.workload == "mix" else GRAD_METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded N(0,1) [N,P] fp32 slab resident in HBM; topology from the "

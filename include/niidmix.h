@@ -60,6 +60,17 @@ enum niidmix_mode {
  * (in-degree + 1) is <= 4 (ring, grid): fewer speculative gathers per batch.  Results unchanged. */
 #define NIIDMIX_FLAG_LOW_DEGREE 4
 
+/* OR-ed into `mode` of niidmix_mix_csr_f32: gradient mean instead of parameter mixing.  Row r's
+ * entries list the nodes whose gradients it averages (val must be 1.0f), in the reference's order:
+ *   acc = +0; acc = fl(acc + g_j) for each entry;  y_r = fl(+0 + fl(acc / row length))
+ * = average_gradients (d_sgd.py:19-27: zeros_like, add_, div_(len(models))) followed by
+ * update_gradients (d_sgd.py:37-45: grad.zero_(); grad.add_(g)).  Used by --clique-gradient (the
+ * clique's members, clique order; with removed clique edges only the members adjacent to the node,
+ * d_sgd.py:56-78) and --unbiased-gradient (topology['neighbourhoods'][rank] order, d_sgd.py:79-90).
+ * Identical results in EXACT and FAST mode (w = 1: fma(1, g, acc) == fl(acc + g)).  Exclusive with
+ * NIIDMIX_FLAG_AVERAGE_ONLY. */
+#define NIIDMIX_FLAG_MEAN 8
+
 /* ABI version (NIIDMIX_ABI_VERSION). */
 int niidmix_abi_version(void);
 
@@ -76,7 +87,7 @@ const char *niidmix_last_error(void);
  *            (the reference's models[0] = self, d_sgd.py:105)
  *   val      [nnz] fp32 weights (device): val = W[src, rank] (d_sgd.py:106), self weight first
  *   mode     NIIDMIX_MODE_EXACT or NIIDMIX_MODE_FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY
- *            | NIIDMIX_FLAG_LOW_DEGREE
+ *            | NIIDMIX_FLAG_LOW_DEGREE | NIIDMIX_FLAG_MEAN
  * Rows with no entries are written as +0. */
 int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                         int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,
@@ -186,6 +197,18 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
  *   mode EXACT reproduces the reference's left-to-right fl(acc + fl(w*x_k)) with w = fp32(1/n). */
 int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, float *mean,
                           double *dist2, int mode, void *stream);
+
+/* Segment gradient mean for --clique-gradient without removed clique edges (d_sgd.py:56-65):
+ * segment s lists the member rows seg_row[seg_ptr[s] .. seg_ptr[s+1]) in clique order, and EVERY
+ * member row of y receives the same mean of the members' rows of g:
+ *   acc = +0; acc = fl(acc + g_m) in member order; y_m = fl(+0 + fl(acc / len))
+ * = average_gradients (d_sgd.py:19-27) + update_gradients (d_sgd.py:37-45), bit for bit.  One read
+ * of every member row and one write (HBM-bound), instead of len gathers per output row.
+ *   g  [*, ld_g] gradient slab (device), y [*, ld_y] output (device, must not overlap g)
+ *   seg_ptr [n_seg+1], seg_row [seg_ptr[n_seg]] int32 (device).  Rows in no segment are untouched. */
+int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t p,
+                                  int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
+                                  void *stream);
 
 /* Strided host <-> device copy (hipMemcpy2DAsync) of `rows` rows of `width_bytes` each, used by
  * the host-resident drop-in (niidmix.slab) to stream column windows of the pinned [N, P] host slab

@@ -120,7 +120,11 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
                                                  const int32_t *__restrict__ col,
                                                  const float *__restrict__ val,
                                                  int64_t n_row_groups, int64_t n_items,
-                                                 int avg_only) {
+                                                 int flags) {
+    // flags: NIIDMIX_FLAG_AVERAGE_ONLY (write acc), NIIDMIX_FLAG_MEAN (gradient mean: acc starts at
+    // +0 instead of x_self*0, result fl(+0 + fl(acc / row length)))
+    const bool avg_only = (flags & NIIDMIX_FLAG_AVERAGE_ONLY) != 0;
+    const bool mean = (flags & NIIDMIX_FLAG_MEAN) != 0;
     constexpr int S = 4 * SPL / VW;           // slots per lane
     constexpr int NE = 4 * SPL;               // columns per lane
     constexpr int64_t CH = kChunk * SPL;      // columns per (row, chunk) work item
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
 #pragma unroll
                     for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xv[u] + q * VW);
                 }
-                if (kb == beg && j == 0) {
+                if (kb == beg && j == 0 && !mean) {
                     // self * 0 (the first entry is the node itself): keeps -0.0, inf/NaN -> NaN
 #pragma unroll
                     for (int e = 0; e < NE; ++e) { z[e] = xv[0][e] * 0.f; acc[e] = z[e]; }
@@ -179,9 +183,16 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
             }
         }
         // update_models: p.mul_(0.); p.add_(new)  ->  z + acc   (AVERAGE_ONLY: acc)
+        // MEAN: average_gradients' g.div_(len) then update_gradients' zero_(); add_(g) (d_sgd.py:19-45)
         float o[NE];
+        if (mean) {
+            const float len = (float)(end > beg ? end - beg : 1);   // empty row: +0 / 1
 #pragma unroll
-        for (int e = 0; e < NE; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+            for (int e = 0; e < NE; ++e) o[e] = 0.f + acc[e] / len;
+        } else {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+        }
         float *dst = y + row * ld_y;
 #pragma unroll
         for (int q = 0; q < S; ++q)
@@ -909,6 +920,66 @@ __global__ __launch_bounds__(256) void k_row_dist2(const float *__restrict__ x, 
     if (threadIdx.x == 0) dist2[row] = part[0];
 }
 
+// ----------------------------------------------------------------------------------------------
+// Segment gradient mean (--clique-gradient without removed edges, d_sgd.py:56-65): every member of
+// a segment (clique) receives the SAME mean of the members' gradients, so each gradient row is read
+// once and each output row written once — HBM-bound, 8 B per node-parameter, like k_mix_clique.
+// Exact: acc = +0 (zeros_like), acc = fl(acc + g_m) in the segment's member order (add_),
+// mean = fl(acc / len) (div_, true division), out = fl(+0 + mean) (update_gradients: zero_(); add_).
+// Work item = (segment, chunk of 256*V columns); 256 threads, V columns per thread; member rows are
+// fetched 64 at a time lane-parallel and handed out by v_readlane; U loads in flight per batch.
+template <int V, int U>
+__global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restrict__ g, int64_t ld_g,
+                                                           float *__restrict__ y, int64_t ld_y,
+                                                           int64_t p, int64_t n_seg,
+                                                           const int32_t *__restrict__ seg_ptr,
+                                                           const int32_t *__restrict__ seg_row,
+                                                           int64_t n_chunks) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t t = blockIdx.x; t < n_seg * n_chunks; t += gridDim.x) {
+        const int64_t seg = t / n_chunks;
+        const int64_t c = (t % n_chunks) * (256 * V) + (int64_t)threadIdx.x * V;
+        const bool ok = c < p;                   // p % V == 0: a thread is all-in or all-out
+        const int64_t cc = ok ? c : 0;           // loads stay unconditional
+        const int beg = seg_ptr[seg], end = seg_ptr[seg + 1];
+        float acc[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = 0.f;
+        for (int kb = beg; kb < end; kb += 64) {
+            const int cnt = end - kb < 64 ? end - kb : 64;
+            const int d_row = seg_row[kb + (lane < cnt ? lane : cnt - 1)];
+            for (int j = 0; j < cnt; j += U) {
+                float v[U][V];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int jj = j + u < cnt ? j + u : cnt - 1;
+                    ldv<V>(g + (int64_t)__builtin_amdgcn_readlane(d_row, jj) * ld_g + cc, v[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (j + u < cnt) {
+#pragma unroll
+                        for (int e = 0; e < V; ++e) acc[e] = acc[e] + v[u][e];
+                    }
+            }
+        }
+        const float len = (float)(end > beg ? end - beg : 1);
+        float o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = 0.f + acc[e] / len;
+        // every lane fetches the descriptors (v_readlane reads lanes that must be active): only
+        // the stores are masked by `ok`
+        for (int kb = beg; kb < end; kb += 64) {
+            const int cnt = end - kb < 64 ? end - kb : 64;
+            const int d_row = seg_row[kb + (lane < cnt ? lane : cnt - 1)];
+            for (int j = 0; j < cnt; ++j) {
+                float *dst = y + (int64_t)__builtin_amdgcn_readlane(d_row, j) * ld_y + c;
+                if (ok) stv_nt<V>(dst, o);
+            }
+        }
+    }
+}
+
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int64_t grid_for(int64_t items) { return items < kMaxGrid ? ((items + 7) / 8) * 8 : kMaxGrid; }
@@ -986,9 +1057,11 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
                         int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,
                         int mode, void *stream) {
     if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
-    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    const int kflags = mode & (NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_MEAN);
     const int low_degree = (mode & NIIDMIX_FLAG_LOW_DEGREE) ? 1 : 0;
-    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE);
+    if ((kflags & NIIDMIX_FLAG_AVERAGE_ONLY) && (kflags & NIIDMIX_FLAG_MEAN))
+        return set_error(NIIDMIX_EINVAL, "AVERAGE_ONLY and MEAN are exclusive");
+    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE | NIIDMIX_FLAG_MEAN);
     if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
         return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
     if (n_rows == 0 || p == 0) return NIIDMIX_OK;
@@ -1009,7 +1082,7 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     const dim3 grid((unsigned)grid_for(n_items)), block(256);
     // gathers in flight per batch: 4 when the caller flags a low-degree graph (ring, grid), else 8
     const bool lowdeg = low_degree != 0;
-#define NIIDMIX_CSR(E, V, S, UU) hipLaunchKernelGGL((k_mix_csr<E, V, S, UU>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, avg_only)
+#define NIIDMIX_CSR(E, V, S, UU) hipLaunchKernelGGL((k_mix_csr<E, V, S, UU>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, kflags)
 #define NIIDMIX_CSR_U(E, V, S) do { if (lowdeg) NIIDMIX_CSR(E, V, S, 4); else NIIDMIX_CSR(E, V, S, 8); } while (0)
 #define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR_U(E, V, 4); else NIIDMIX_CSR_U(E, V, 1); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) {
@@ -1183,6 +1256,29 @@ int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
     if (rc != NIIDMIX_OK || !dist2) return rc;
     hipLaunchKernelGGL(k_row_dist2, dim3((unsigned)n), dim3(256), 0, s, x, ld_x, p, mean, dist2);
     return check_launch("k_row_dist2");
+}
+
+int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t p,
+                                  int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
+                                  void *stream) {
+    if (p < 0 || n_seg < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n_seg == 0 || p == 0) return NIIDMIX_OK;
+    if (!g || !y || !seg_ptr || !seg_row) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_g < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (g == y) return set_error(NIIDMIX_EALIAS, "g and y alias: the mean is out-of-place");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool vec4 = p % 4 == 0 && ld_g % 4 == 0 && ld_y % 4 == 0 && aligned16(g) && aligned16(y);
+    const int64_t cols = vec4 ? 1024 : 256;
+    const int64_t n_chunks = (p + cols - 1) / cols;
+    const int64_t n_items = n_seg * n_chunks;
+    const dim3 grid((unsigned)(n_items < kMaxGrid ? n_items : kMaxGrid)), block(256);
+    if (vec4)
+        hipLaunchKernelGGL((k_grad_segment_mean<4, 8>), grid, block, 0, s, g, ld_g, y, ld_y, p, n_seg,
+                           seg_ptr, seg_row, n_chunks);
+    else
+        hipLaunchKernelGGL((k_grad_segment_mean<1, 16>), grid, block, 0, s, g, ld_g, y, ld_y, p, n_seg,
+                           seg_ptr, seg_row, n_chunks);
+    return check_launch("k_grad_segment_mean");
 }
 
 int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,

@@ -55,6 +55,8 @@ SIGNATURES = {
                                             ctypes.POINTER(TilePlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
+    "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp,
+                                                     _vp]),
     "niidmix_copy2d_async": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp]),
     "niidmix_stream_copy_f32": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
 }

@@ -17,7 +17,8 @@ kernels mix it (niidmix.ops.Mixer).  Mixing mode (params['algorithm']['mixing-mo
 NIIDMIX_MODE environment variable):
   'exact' (default)  bit-identical to the reference loop (tests/test_gpu_dropin.py)
   'fast'             clique-factored / MFMA kernels, within 1e-5 condition-aware relative
-Local training, gradient variants and sampling stay on the CPU exactly as in the reference.
+Gradient averaging (--clique-gradient, --unbiased-gradient) also runs on the GPU, bit-identical
+(niidmix.gradient); local training, optimizer steps and sampling stay on the CPU as in the reference.
 """
 import argparse
 import itertools
@@ -37,7 +38,8 @@ MODULE = "niidmix.d_sgd"
 
 
 # ------------------------------------------------------------------------------------------------
-# gradient helpers (CPU, as the reference)
+# gradient helpers: the reference module's CPU functions, kept for API compatibility (callers that
+# import them directly); gradient() below runs the averaged variants on the GPU
 def average_gradients(models):
     """Mean of the models' gradients (d_sgd.py:19-27): zeros, add every grad, divide by count."""
     with torch.no_grad():
@@ -72,40 +74,63 @@ def update_gradients(models, gradients):
     return models
 
 
-def gradient(nodes, topology, params):
-    """Apply the local, clique-averaged or unbiased gradient, then step (d_sgd.py:47-94)."""
+def _averages_gradients(params):
     alg = params["algorithm"]
-    if not alg["clique-gradient"] and not alg["unbiased-gradient"]:
+    return bool(alg.get("clique-gradient") or alg.get("unbiased-gradient"))
+
+
+class _GradEngine:
+    """Gradient NodeSlab + GradMean + SlabMixer for one (node list, topology, flags) triple."""
+
+    def __init__(self, nodes, topology, params, device):
+        from .gradient import GradMean, build_grad_plan
+        from .slab import NodeSlab, SlabMixer
+        self.topology = topology
+        self.key = _grad_key(params)
+        self.plan = build_grad_plan(len(nodes), topology, params)
+        self.slab = NodeSlab([n["model"] for n in nodes], grads=True)
+        self.op = GradMean(self.plan, device)
+        self.runner = SlabMixer(self.op, self.slab.n, self.slab.p, device,
+                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 16)))
+
+    def valid_for(self, nodes, topology, params):
+        return (topology is self.topology and _grad_key(params) == self.key
+                and self.slab.owns([n["model"] for n in nodes]))
+
+
+def _grad_key(params):
+    alg = params["algorithm"]
+    return (bool(alg.get("clique-gradient")), bool(alg.get("unbiased-gradient")),
+            params.get("topology", {}).get("remove-clique-edges", 0))
+
+
+_grad_engines = {}
+
+
+def gradient(nodes, topology, params):
+    """Apply the local, clique-averaged or unbiased gradient, then step (d_sgd.py:47-94).
+
+    The averaged variants run on the GPU: the nodes' gradients are views of one pinned host slab
+    (NodeSlab(grads=True)), streamed through HBM in column windows and averaged by
+    k_grad_segment_mean (whole cliques) or k_mix_csr | NIIDMIX_FLAG_MEAN (removed clique edges,
+    neighbourhoods), bit-identical to average_gradients + update_gradients; the optimizer steps stay
+    on the CPU, on the nodes the reference steps (niidmix.gradient.GradPlan.stepped)."""
+    logging.info("  applying gradients")
+    if not _averages_gradients(params):
         for n in nodes:
             n["optimizer"].step()
         return
-    with torch.no_grad():
-        if alg["clique-gradient"]:
-            removed = params["topology"].get("remove-clique-edges", 0)
-            edges = topology["edges"]
-            for clique in topology["cliques"]:
-                if not removed:
-                    members = [nodes[r]["model"] for r in clique]
-                    update_gradients(members, average_gradients(members))
-                    for r in clique:
-                        nodes[r]["optimizer"].step()
-                else:
-                    grads = {}
-                    for r in clique:
-                        peers = [nodes[q]["model"] for q in clique if q == r or q in edges[r]]
-                        grads[r] = average_gradients(peers)
-                    for r in clique:
-                        update_gradients([nodes[r]["model"]], grads[r])
-                        nodes[r]["optimizer"].step()
-        elif alg["unbiased-gradient"]:
-            hoods = topology["neighbourhoods"]
-            grads = {n["rank"]: average_gradients([nodes[q]["model"] for q in hoods[n["rank"]]])
-                     for n in nodes}
-            for n in nodes:
-                update_gradients([n["model"]], grads[n["rank"]])
-                n["optimizer"].step()
-        else:
-            raise Exception("Invalid execution path, previous cases should cover all possibilities.")
+    key = id(nodes)
+    eng = _grad_engines.get(key)
+    if eng is None or not eng.valid_for(nodes, topology, params):
+        dev = torch.device("cuda", torch.cuda.current_device())
+        eng = _GradEngine(nodes, topology, params, dev)
+        _grad_engines.clear()
+        _grad_engines[key] = eng
+    logging.info("  averaging gradients (GPU, %s)", eng.plan.kind)
+    eng.runner.mix(eng.slab.host)
+    for r in eng.plan.stepped:
+        nodes[r]["optimizer"].step()
 
 
 # ------------------------------------------------------------------------------------------------
@@ -221,7 +246,9 @@ def next_step(state, params, rundir):
     losses, epoch_done = {}, {}
     for node in active:                                   # local training (CPU)
         data, target = next(node["train-iterator"])
-        node["optimizer"].zero_grad()
+        # gradient averaging keeps .grad as views of the pinned gradient slab: zero in place (the
+        # reference's torch 1.7.1 zero_grad behaviour) so backward accumulates into the views
+        node["optimizer"].zero_grad(set_to_none=not _averages_gradients(params))
         loss = F.nll_loss(node["model"].forward(data, params), target)
         loss.backward()
         losses[node["rank"]] = loss.tolist()

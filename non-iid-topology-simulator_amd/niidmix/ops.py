@@ -6,6 +6,8 @@ Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
              max_clique, max_clique_res)            k_mix_clique_wave (fast, HBM-bound)
   mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
+  grad_segment_mean(g, seg_ptr, seg_row, out)       k_grad_segment_mean (clique gradient mean)
+  mix_csr(..., mode | MEAN)                         per-row gradient mean (unbiased / removed edges)
 All ops launch on torch's current HIP stream of the input's device, never synchronise, and raise
 RuntimeError (TORCH_CHECK-style) on bad arguments.  They accept HIP tensors only: there is no CPU
 implementation and no fallback.
@@ -25,6 +27,7 @@ from .topology import MixCSR, to_csr
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
 AVERAGE_ONLY = 2
 LOW_DEGREE = 4
+MEAN = 8
 
 
 def _stream(t):
@@ -197,6 +200,22 @@ def mean_rows(x: torch.Tensor, mean: torch.Tensor, dist2: torch.Tensor, mode: in
                                         mean.data_ptr(), dist2.data_ptr() if want_d else None,
                                         int(mode), _stream(x))
     _lib.check(rc, "niidmix::mean_rows")
+
+
+@torch.library.custom_op("niidmix::grad_segment_mean", mutates_args=("out",))
+def grad_segment_mean(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: torch.Tensor,
+                      out: torch.Tensor) -> None:
+    _slab("g", g)
+    _slab("out", out, cols=g.shape[1])
+    dev = g.device
+    _req(out.device == dev, "g and out must be on the same device")
+    _vec("seg_ptr", seg_ptr, torch.int32, dev)
+    _vec("seg_row", seg_row, torch.int32, dev)
+    _no_overlap(g, out)
+    rc = _lib.lib.niidmix_grad_segment_mean_f32(g.data_ptr(), _ld(g), out.data_ptr(), _ld(out),
+                                                g.shape[1], seg_ptr.numel() - 1,
+                                                seg_ptr.data_ptr(), seg_row.data_ptr(), _stream(g))
+    _lib.check(rc, "niidmix::grad_segment_mean")
 
 
 # ------------------------------------------------------------------------------------------------

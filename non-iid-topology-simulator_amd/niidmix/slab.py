@@ -27,9 +27,16 @@ def _flat_shapes(model):
 
 
 class NodeSlab:
-    """Parameters of `models` as views into one fp32 [N, P] host slab (pinned by default)."""
+    """Parameters of `models` as views into one fp32 [N, P] host slab (pinned by default).
 
-    def __init__(self, models, pin=True):
+    grads=True backs the parameters' .grad tensors instead (the gradient slab of --clique-gradient /
+    --unbiased-gradient, niidmix.gradient): each p.grad becomes a view of the slab, initialised from
+    the current gradient (zeros where there is none).  The views survive training rounds as long as
+    gradients are zeroed in place (optimizer.zero_grad(set_to_none=False), the reference's torch
+    1.7.1 behaviour): backward then accumulates into the existing .grad (0 + g).
+    """
+
+    def __init__(self, models, pin=True, grads=False):
         models = list(models)
         if not models:
             raise ValueError("NodeSlab needs at least one model")
@@ -42,6 +49,7 @@ class NodeSlab:
                     raise ValueError("the mixing kernels are fp32; got a %s parameter" % q.dtype)
         self.models = models
         self.shapes = shapes
+        self.grads = grads
         self.n = len(models)
         self.p = sum(k for _, k in shapes)
         pin = pin and torch.cuda.is_available()
@@ -51,8 +59,15 @@ class NodeSlab:
                 off = 0
                 for q, (shape, k) in zip(m.parameters(), shapes):
                     view = self.host[i, off:off + k]
-                    view.copy_(q.detach().reshape(-1))
-                    q.data = view.view(shape)
+                    if grads:
+                        if q.grad is None:
+                            view.zero_()
+                        else:
+                            view.copy_(q.grad.detach().reshape(-1))
+                        q.grad = view.view(shape)
+                    else:
+                        view.copy_(q.detach().reshape(-1))
+                        q.data = view.view(shape)
                     off += k
 
     def owns(self, models):
@@ -63,9 +78,11 @@ class NodeSlab:
         for i, m in enumerate(models):
             if m is not self.models[i]:
                 return False
-            q = next(iter(m.parameters()), None)
-            if q is not None and q.data_ptr() != base + i * self.p * 4:
-                return False
+            for q in m.parameters():
+                t = q.grad if self.grads else q
+                if t is None or t.data_ptr() != base + i * self.p * 4:
+                    return False
+                break
         return True
 
 

@@ -66,3 +66,25 @@ void oracle_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
         mean[c] = acc;
     }
 }
+
+/* Gradient mean (the --clique-gradient / --unbiased-gradient path): row r of g_out is the mean of
+ * the gradients its CSR row lists, in the reference's order:
+ *   average_gradients (d_sgd.py:19-27): acc = zeros_like (+0); acc.add_(g_j) per model; div_(len)
+ *   update_gradients  (d_sgd.py:37-45): grad.zero_(); grad.add_(mean)   ->  +0 + mean
+ * Rows with no entries are written as +0. */
+void oracle_grad_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t r0,
+                          int64_t r1, int64_t c0, int64_t c1, const int64_t *row_ptr,
+                          const int32_t *col) {
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+        float *out = y + r * ld_y;
+        const float len = (float)(end > beg ? end - beg : 1);
+        for (int64_t c = c0; c < c1; ++c) {
+            float acc = 0.0f;
+            for (int64_t k = beg; k < end; ++k) acc = acc + g[(int64_t)col[k] * ld_g + c];
+            const float mean = acc / len;
+            out[c] = 0.0f + mean;
+        }
+    }
+}

@@ -15,6 +15,9 @@ Contents
                       reference's order; small sizes only.
   mix_exact_c         the same in C (oracle/mix_oracle.c, OpenMP), on any row/column window.
   mean_rows_np/_c     setup.model.average(models) with weights=None (model/__init__.py:15-25).
+  grad_mean_np/_c     average_gradients + update_gradients (d_sgd.py:19-27,37-45) over a CSR whose
+                      row r lists the nodes whose gradients node r averages (--clique-gradient,
+                      --unbiased-gradient; d_sgd.py:47-94).
   reference_loop_average   a faithful restatement of the reference's module-level loop (per-node
                       deepcopy, mul_(0), add_(w*p), then update_models), used as the CPU baseline
                       ("kind": "port") in bench.py.
@@ -57,6 +60,23 @@ def mix_exact_np(x, row_ptr, col, val, average_only=False):
     return y
 
 
+def grad_mean_np(g, row_ptr, col):
+    """acc = zeros_like (+0); acc.add_(g_j) in row order; div_(len) (true fp32 division, not a
+    reciprocal multiply); then the target grad is zero_() + add_(mean) -> +0 + mean
+    (d_sgd.py:19-27 average_gradients, d_sgd.py:37-45 update_gradients).  Empty rows -> +0."""
+    g = np.asarray(g, np.float32)
+    n = len(row_ptr) - 1
+    y = np.empty((n, g.shape[1]), np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        for r in range(n):
+            b, e = int(row_ptr[r]), int(row_ptr[r + 1])
+            acc = np.zeros(g.shape[1], np.float32)
+            for k in range(b, e):
+                acc = acc + g[col[k]]
+            y[r] = np.float32(0.0) + acc / np.float32(max(e - b, 1))
+    return y
+
+
 def mean_rows_np(x):
     """setup.model.average(models) with weights=None: w = float(1./K) applied in fp32."""
     x = np.asarray(x, np.float32)
@@ -85,6 +105,8 @@ def c_lib(build=True):
     lib.oracle_mix_csr_f32.restype = None
     lib.oracle_mean_rows_f32.argtypes = [vp, i64, i64, i64, vp]
     lib.oracle_mean_rows_f32.restype = None
+    lib.oracle_grad_mean_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64, i64, vp, vp]
+    lib.oracle_grad_mean_f32.restype = None
     _c = lib
     return lib
 
@@ -107,6 +129,22 @@ def mix_exact_c(x, row_ptr, col, val, rows=None, cols=None, average_only=False, 
         out = np.zeros((n, x.shape[1]), np.float32)
     lib.oracle_mix_csr_f32(_ptr(x), x.shape[1], _ptr(out), out.shape[1], r0, r1, c0, c1,
                            _ptr(row_ptr), _ptr(col), _ptr(val), int(bool(average_only)))
+    return out
+
+
+def grad_mean_c(g, row_ptr, col, rows=None, cols=None, out=None):
+    """C restatement of grad_mean_np on output rows [r0, r1) and columns [c0, c1)."""
+    lib = c_lib()
+    g = np.ascontiguousarray(g, np.float32)
+    row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    n = len(row_ptr) - 1
+    r0, r1 = rows if rows is not None else (0, n)
+    c0, c1 = cols if cols is not None else (0, g.shape[1])
+    if out is None:
+        out = np.zeros((n, g.shape[1]), np.float32)
+    lib.oracle_grad_mean_f32(_ptr(g), g.shape[1], _ptr(out), out.shape[1], r0, r1, c0, c1,
+                             _ptr(row_ptr), _ptr(col))
     return out
 
 
@@ -187,3 +225,25 @@ def reference_loop_average(nodes, topology):
             for mp, newp in zip(nd["model"].parameters(), results[nd["rank"]].parameters()):
                 mp.mul_(0.)
                 mp.add_(newp)
+
+
+def reference_loop_clique_gradient(nodes, cliques):
+    """d_sgd.gradient with --clique-gradient and no removed edges (d_sgd.py:56-65) as the
+    reference runs it, minus the optimizer steps: per clique, average_gradients (zeros_like, add_
+    every member's grad, div_(len), d_sgd.py:19-27) then update_gradients on every member
+    (grad.zero_(); grad.add_(mean), d_sgd.py:37-45).  torch CPU; the CPU baseline of
+    bench.py --workload grad-clique."""
+    import torch
+    with torch.no_grad():
+        for clique in cliques:
+            models = [nodes[r]["model"] for r in clique]
+            acc = [torch.zeros_like(q.grad.data) for q in models[0].parameters()]
+            for mdl in models:
+                for a, q in zip(acc, mdl.parameters()):
+                    a.add_(q.grad.data)
+            for a in acc:
+                a.div_(len(models))
+            for mdl in models:
+                for a, q in zip(acc, mdl.parameters()):
+                    q.grad.data.zero_()
+                    q.grad.data.add_(a)

@@ -25,7 +25,25 @@ def pytest_configure(config):
 
 def golden_cases(pattern=""):
     names = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
-    return [n for n in names if pattern in n and not n.startswith("uniform_avg")]
+    return [n for n in names if pattern in n and not n.startswith(("uniform_avg", "grad_"))]
+
+
+def grad_cases():
+    """Gradient-averaging fixtures (tests/golden/grad_*.npz, d_sgd.gradient run by make_golden.py)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("grad_") and f.endswith(".npz"))
+
+
+def load_grad(name):
+    """(fixture arrays, topology with int keys as setup.topology.load returns it, params)."""
+    import json
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    out = {k: d[k] for k in d.files}
+    topo = json.loads(str(out["topology_json"]))
+    topo["edges"] = {int(r): v for r, v in topo["edges"].items()}
+    if "neighbourhoods" in topo:
+        topo["neighbourhoods"] = {int(r): v for r, v in topo["neighbourhoods"].items()}
+    params = json.loads(str(out["params_json"]))
+    return out, topo, params
 
 
 def load_golden(name):

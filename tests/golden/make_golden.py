@@ -22,6 +22,14 @@ Saved per case (tests/golden/<case>.npz):
                       val = W[i,i], W[src,i] ...   (d_sgd.py:105-110)
   cliques_flat, cliques_ptr   (d-cliques cases only)
   shapes_json    parameter shapes of the model (multi-tensor case)
+Gradient cases (tests/golden/grad_<case>.npz) run the reference's `d_sgd.gradient`
+(d_sgd.py:47-94: --clique-gradient with and without removed clique edges, --unbiased-gradient)
+on nodes whose models carry seeded parameters AND seeded .grad tensors, with the reference's own
+optimizer (d_sgd.optimizer: SGD lr 0.1, momentum 0), and store
+  x, g           fp32 [N, P] parameters / gradients before
+  y, g_out       fp32 [N, P] parameters / gradients after
+  topology_json  {"edges", "cliques"?, "neighbourhoods"?} (no weights: gradient() never reads them)
+  params_json    the 'algorithm' and 'topology' params passed
 Small cases additionally keep the raw topology.json (tests/golden/<case>.topology.json) so the
 build's own reader can be checked against the reference loader's output.
 
@@ -168,6 +176,90 @@ def dcliques(n, size, interclique, seed=1337, remove=0):
     return {rank: list(edges[rank]) for rank in edges}, [list(c) for c in cl]
 
 
+def _flat(nodes, attr):
+    out = []
+    for nd in nodes:
+        ts = [p.grad if attr == "grad" else p for p in nd["model"].parameters()]
+        out.append(torch.cat([t.detach().reshape(-1) for t in ts]).numpy())
+    return np.stack(out)
+
+
+def save_grad_case(name, n, p, topo, alg, remove=0, shapes=None, seed=0, special=False):
+    """Run the reference's d_sgd.gradient on seeded parameters + gradients (see module doc)."""
+    shapes = shapes or [(p,)]
+    assert sum(int(np.prod(s)) for s in shapes) == p
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, p, generator=gen).numpy()
+    g = torch.randn(n, p, generator=gen).numpy()
+    if special:
+        g[0, 0] = np.inf; g[1, 1] = -np.inf; g[2, 2] = np.nan
+        g[:, 3] = -0.0; g[0, 4] = -0.0; g[1, 5] = 3.0e38; g[2, 5] = 3.0e38; g[3, 6] = 1e-45
+        x[:, 3] = -0.0
+    params = {"algorithm": {"clique-gradient": alg == "clique", "unbiased-gradient": alg == "unbiased",
+                            "learning-rate": 0.1, "learning-momentum": 0.0},
+              "topology": {"remove-clique-edges": remove}}
+    nodes = []
+    for rank in range(n):
+        m = FlatModel(shapes)
+        off = 0
+        with torch.no_grad():
+            for q in m.parameters():
+                k = q.numel()
+                q.copy_(torch.from_numpy(x[rank, off:off + k].copy()).view_as(q))
+                q.grad = torch.from_numpy(g[rank, off:off + k].copy()).view_as(q).clone()
+                off += k
+        nodes.append({"rank": rank, "model": m, "optimizer": R.d_sgd.optimizer(m, params)})
+    text = json.dumps(topo)
+    loaded = json.loads(text)
+    loaded["edges"] = {int(r): loaded["edges"][r] for r in loaded["edges"]}
+    if "neighbourhoods" in loaded:
+        loaded["neighbourhoods"] = {int(r): loaded["neighbourhoods"][r] for r in loaded["neighbourhoods"]}
+    R.d_sgd.gradient(nodes, loaded, params)
+    np.savez_compressed(os.path.join(OUT, "grad_" + name + ".npz"), x=x, g=g, y=_flat(nodes, "data"),
+                        g_out=_flat(nodes, "grad"), topology_json=np.asarray(text),
+                        params_json=np.asarray(json.dumps(params)),
+                        shapes_json=np.asarray(json.dumps([list(s) for s in shapes])))
+    print(f"grad_{name}: N={n} P={p} {alg} remove={remove}")
+
+
+def grad_cases():
+    e, cl = dcliques(300, 30, "fully-connected")
+    save_grad_case("dcliques300_fc_p37", 300, 37, {"edges": e, "cliques": cl}, "clique")
+    e, cl = dcliques(1000, 100, "fully-connected")
+    save_grad_case("dcliques1000_fc_p64", 1000, 64, {"edges": e, "cliques": cl}, "clique", seed=1)
+    e, cl = dcliques(200, 20, "fractal", remove=5)
+    save_grad_case("dcliques200_fractal_rm5_p40", 200, 40, {"edges": e, "cliques": cl}, "clique",
+                   remove=5, seed=2)
+    e, cl = dcliques(40, 10, "ring")
+    save_grad_case("dcliques40_ring_special_p16", 40, 16, {"edges": e, "cliques": cl}, "clique",
+                   seed=3, special=True)
+    save_grad_case("dcliques40_ring_rm3_special_p16", 40, 16,
+                   {"edges": dcliques(40, 10, "ring", remove=3)[0],
+                    "cliques": dcliques(40, 10, "ring", remove=3)[1]}, "clique", remove=3, seed=4,
+                   special=True)
+    # 2 cliques of 2 with the linear MNIST model ([10,784] + [10]): flattening order of gradients
+    save_grad_case("cliques4_linear7850", 4, 7850, {"edges": {0: [1], 1: [0, 2], 2: [3, 1], 3: [2]},
+                                                   "cliques": [[1, 0], [2, 3]]}, "clique",
+                   shapes=[(10, 784), (10,)], seed=5)
+    # unbiased gradient: neighbourhoods of 1..9 nodes in shuffled order (incl. the node itself or
+    # not), over a ring; the reference generators of this repo version do not emit neighbourhoods
+    import random
+    rnd = random.Random(1337)
+    n = 100
+    edges = R.ring.create(_nodes(n), R.metrics.random({"seed": 1337}))
+    hoods = {}
+    for r in range(n):
+        k = rnd.randint(1, 9)
+        hoods[r] = rnd.sample(range(n), k)
+    save_grad_case("unbiased_ring100_p257", n, 257,
+                   {"edges": {r: list(edges[r]) for r in edges}, "neighbourhoods": hoods},
+                   "unbiased", seed=6)
+    hoods8 = {r: rnd.sample(range(8), rnd.randint(1, 8)) for r in range(8)}
+    save_grad_case("unbiased_n8_special_p16", 8, 16,
+                   {"edges": {r: [(r + 1) % 8, (r - 1) % 8] for r in range(8)},
+                    "neighbourhoods": hoods8}, "unbiased", seed=7, special=True)
+
+
 def main():
     # 1) ring N=100, P=257 (odd tail), random metric, MH weights 1/3
     edges = R.ring.create(_nodes(100), R.metrics.random({"seed": 1337}))
@@ -237,4 +329,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--grad" in sys.argv:
+        grad_cases()
+    else:
+        main()
+        grad_cases()

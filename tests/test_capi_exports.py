@@ -42,8 +42,10 @@ def test_argument_errors_without_gpu():
     assert rc == _lib.EINVAL and b"null" in L.niidmix_last_error()
     rc = L.niidmix_mix_csr_f32(16, 4, 16, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EALIAS
-    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 9, None)
-    assert rc == _lib.EINVAL
+    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 16, None)
+    assert rc == _lib.EINVAL        # unknown mode
+    rc = L.niidmix_mix_csr_f32(16, 4, 1024, 4, 1, 4, 8, 8, 8, 2 | 8, None)
+    assert rc == _lib.EINVAL        # AVERAGE_ONLY and MEAN are exclusive
     rc = L.niidmix_mix_csr_f32(16, 2, 1024, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EINVAL        # ld < p
     assert L.niidmix_mix_csr_f32(16, 4, 1024, 4, 0, 4, 8, 8, 8, 0, None) == _lib.OK  # empty
@@ -65,6 +67,10 @@ def test_argument_errors_without_gpu():
     tp = _lib.TilePlanC(1, 16, 0, 8, 8, 8, 8, 8, 8)
     assert L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 9, None) == _lib.EINVAL
     assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
+    assert L.niidmix_grad_segment_mean_f32(None, 4, 16, 4, 4, 1, 8, 8, None) == _lib.EINVAL
+    assert L.niidmix_grad_segment_mean_f32(16, 4, 16, 4, 4, 1, 8, 8, None) == _lib.EALIAS
+    assert L.niidmix_grad_segment_mean_f32(16, 2, 1024, 4, 4, 1, 8, 8, None) == _lib.EINVAL
+    assert L.niidmix_grad_segment_mean_f32(16, 4, 1024, 4, 4, 0, 8, 8, None) == _lib.OK
     rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
     assert rc == _lib.EINVAL
     assert L.niidmix_stream_copy_f32(16, 1024, 6, None) == _lib.EUNSUPPORTED   # n % 4
