@@ -162,11 +162,14 @@ int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  *   sub_ptr    [n_sub+1] int64 offsets into the position arrays
  *   sub_rows   [n_sub*rt] int32 output rows, -1 for an unused slot
  *   sub_wself  [n_sub*rt] fp32 W[r, r] of each tile row (its first CSR entry)
- *   pos_src    [L] int32 source row of every position
+ *   pos_src    [L] int32 source row of every position, | NIIDMIX_TILE_POS_UNIFORM when every
+ *              slot of the position's pos_w holds the same fp32 value (exact mode then forms the
+ *              product fl(w*x) once per position and adds it to each taking row: same bits)
  *   pos_mask   [L] uint32: bit r set when tile row r takes the position (unused slots: set)
  *   pos_w      [L*rt] fp32 weight W[src, row] per tile row (0 where the row skips the position)
  *   (pos_* must be valid device pointers even when L == 0; they are read only inside sub_ptr ranges)
  * mode: NIIDMIX_MODE_EXACT / _FAST, optionally | NIIDMIX_FLAG_AVERAGE_ONLY. */
+#define NIIDMIX_TILE_POS_UNIFORM (1 << 30)
 typedef struct niidmix_tile_plan {
     int64_t n_sub;
     int32_t rt;
@@ -181,6 +184,38 @@ typedef struct niidmix_tile_plan {
 
 int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                          const niidmix_tile_plan *plan, int mode, void *stream);
+
+/* LDS-staged merged-order row tiles (exact-mode default for clique topologies): the same tiles and
+ * results as niidmix_mix_tile_f32 (bit for bit in NIIDMIX_MODE_EXACT), grouped: a group (a clique)
+ * owns consecutive tiles and a list of the DISTINCT source rows its tiles read.  One workgroup per
+ * (group, 128-column chunk) stages those rows' columns in LDS (one HBM read per row), then each
+ * wave applies one tile's positions from LDS.  Built by niidmix.tile.build_tile_lds_plan.
+ *   rt, n_sub, sub_ptr, sub_rows, sub_wself, pos_mask, pos_w   as niidmix_tile_plan
+ *   pos_slot     [L] int32 index of the position's source in its group's grp_src_rows list
+ *                (| NIIDMIX_TILE_POS_UNIFORM as for niidmix_tile_plan.pos_src)
+ *   sub_slot     [n_sub*rt] int32 index of each tile row's own row in the group list (0 for unused)
+ *   n_grp        groups;  grp_tile_ptr [n_grp+1] int32 tile ranges;  max_tiles = most tiles in a
+ *                group: 1..16 for rt 8, 1..8 for rt 16, 1..4 for rt 32 (64*max_tiles threads)
+ *   grp_src_ptr  [n_grp+1] int32;  grp_src_rows  int32 source rows;  max_src = largest list (<= 256:
+ *                max_src * 512 B of LDS)
+ * Needs even p and ld and 8-B aligned slabs (2 columns per lane).  mode as niidmix_mix_tile_f32. */
+typedef struct niidmix_tile_lds_plan {
+    int64_t n_sub;
+    int32_t rt, n_grp, max_src, max_tiles;
+    const int64_t *sub_ptr;
+    const int32_t *sub_rows;
+    const int32_t *sub_slot;
+    const float *sub_wself;
+    const int32_t *pos_slot;
+    const uint32_t *pos_mask;
+    const float *pos_w;
+    const int32_t *grp_tile_ptr;
+    const int32_t *grp_src_ptr;
+    const int32_t *grp_src_rows;
+} niidmix_tile_lds_plan;
+
+int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                             const niidmix_tile_lds_plan *plan, int mode, void *stream);
 
 /* Dense mixing Y = W^T X on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), for topologies dense
  * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).

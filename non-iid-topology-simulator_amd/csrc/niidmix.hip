@@ -749,6 +749,27 @@ __global__ __launch_bounds__(256) void k_mix_staged(
 // mul+add per lane for one NE-column load: VALU-bound, not gather-bound.  Weights come in by
 // scalar loads (uniform per position), the source row / mask lane-parallel by v_readlane.  A
 // position every row takes (mask == FULL) skips the per-row select.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Packed (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32) forms of axpy on 2 columns.  Per component
+// these are the same IEEE roundings as the scalar forms (exact: fl(acc + fl(w*x)), no contraction).
+template <bool EXACT>
+__device__ __forceinline__ f2 axpy2(float w, f2 xv, f2 acc) {
+    if constexpr (EXACT) {
+        const f2 t = xv * w;
+        return acc + t;
+    } else {
+        return __builtin_elementwise_fma((f2){w, w}, xv, acc);
+    }
+}
+
+// Position flag in pos_src (bit 30, NIIDMIX_TILE_POS_UNIFORM): every tile row's weight for this
+// position is the same fp32 value (pos_w[pos*RT + r] == pos_w[pos*RT] for all r).  Exact mode then
+// forms the product fl(w*x) ONCE and adds it to each taking row — the same bits as per-row products
+// — so a position costs NE/2 packed muls + (rows taking it)*NE/2 packed adds per lane.
+constexpr int kPosUniform = 1 << 30;
+constexpr int kPosRowMask = kPosUniform - 1;
+
 template <bool EXACT, int VW, int NE, int RT>
 __global__ __launch_bounds__(256) void k_mix_tile(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
@@ -757,9 +778,11 @@ __global__ __launch_bounds__(256) void k_mix_tile(
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w,
     int64_t n_sub_groups, int64_t n_items, int avg_only) {
     constexpr int S = NE / VW;                  // slots per lane
+    constexpr int NH = NE / 2;                  // packed column pairs per lane
     constexpr int64_t CW = 64 * NE;             // columns per work item
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                        // positions whose loads are in flight together
+    static_assert(NE % 2 == 0, "NE must be even (packed pairs)");
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
     for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
@@ -780,7 +803,7 @@ __global__ __launch_bounds__(256) void k_mix_tile(
         const int li = lane < RT ? lane : RT - 1;
         const int d_row = sub_rows[sub * RT + li];
         const float d_ws = sub_wself[sub * RT + li];
-        float acc[RT][NE];
+        f2 acc[RT][NH];
         // first entry of every row: the node itself (acc = x*0; acc += w_self*x)
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
@@ -791,7 +814,10 @@ __global__ __launch_bounds__(256) void k_mix_tile(
             for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xs + q * VW);
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
 #pragma unroll
-            for (int e = 0; e < NE; ++e) acc[r][e] = axpy<EXACT>(ws, xs[e], xs[e] * 0.f);
+            for (int h = 0; h < NH; ++h) {
+                const f2 xx = {xs[2 * h], xs[2 * h + 1]};
+                acc[r][h] = axpy2<EXACT>(ws, xx, xx * 0.f);
+            }
         }
         const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
         for (int64_t kb = beg; kb < end; kb += 64) {
@@ -804,7 +830,8 @@ __global__ __launch_bounds__(256) void k_mix_tile(
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     const int jj = j + u < cnt ? j + u : cnt - 1;     // clamped: loads unconditional
-                    const float *src = x + (int64_t)__builtin_amdgcn_readlane(d_src, jj) * ld_x;
+                    const int srow = __builtin_amdgcn_readlane(d_src, jj) & kPosRowMask;
+                    const float *src = x + (int64_t)srow * ld_x;
 #pragma unroll
                     for (int q = 0; q < S; ++q) ldv<VW>(src + cs[q], xv[u] + q * VW);
                 }
@@ -812,25 +839,44 @@ __global__ __launch_bounds__(256) void k_mix_tile(
                 for (int u = 0; u < D; ++u) {
                     if (j + u >= cnt) break;
                     const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                    const bool uni = (__builtin_amdgcn_readlane(d_src, j + u) & kPosUniform) != 0;
                     const float *wp = pos_w + (kb + j + u) * RT;
-                    if (m == FULL) {
+                    f2 xx[NH];
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) xx[h] = (f2){xv[u][2 * h], xv[u][2 * h + 1]};
+                    if (EXACT && uni) {
+                        const float w = wp[0];
+                        f2 tp[NH];
+#pragma unroll
+                        for (int h = 0; h < NH; ++h) tp[h] = xx[h] * w;
+                        if (m == FULL) {
+#pragma unroll
+                            for (int r = 0; r < RT; ++r)
+#pragma unroll
+                                for (int h = 0; h < NH; ++h) acc[r][h] = acc[r][h] + tp[h];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < RT; ++r)
+                                if ((m >> r) & 1u) {                       // wave-uniform
+#pragma unroll
+                                    for (int h = 0; h < NH; ++h) acc[r][h] = acc[r][h] + tp[h];
+                                }
+                        }
+                    } else if (m == FULL) {
 #pragma unroll
                         for (int r = 0; r < RT; ++r) {
                             const float w = wp[r];
 #pragma unroll
-                            for (int e = 0; e < NE; ++e) acc[r][e] = axpy<EXACT>(w, xv[u][e], acc[r][e]);
+                            for (int h = 0; h < NH; ++h) acc[r][h] = axpy2<EXACT>(w, xx[h], acc[r][h]);
                         }
                     } else {
 #pragma unroll
-                        for (int r = 0; r < RT; ++r) {
-                            const float w = wp[r];
-                            const bool take = (m >> r) & 1u;
+                        for (int r = 0; r < RT; ++r)
+                            if ((m >> r) & 1u) {                           // wave-uniform
+                                const float w = wp[r];
 #pragma unroll
-                            for (int e = 0; e < NE; ++e) {
-                                const float v = axpy<EXACT>(w, xv[u][e], acc[r][e]);
-                                acc[r][e] = take ? v : acc[r][e];
+                                for (int h = 0; h < NH; ++h) acc[r][h] = axpy2<EXACT>(w, xx[h], acc[r][h]);
                             }
-                        }
                     }
                 }
             }
@@ -847,7 +893,10 @@ __global__ __launch_bounds__(256) void k_mix_tile(
 #pragma unroll
                 for (int q = 0; q < S; ++q) ldv<VW>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cs[q], xs + q * VW);
 #pragma unroll
-                for (int e = 0; e < NE; ++e) acc[r][e] = xs[e] * 0.f + acc[r][e];
+                for (int h = 0; h < NH; ++h) {
+                    const f2 xx = {xs[2 * h], xs[2 * h + 1]};
+                    acc[r][h] = xx * 0.f + acc[r][h];
+                }
             }
         }
 #pragma unroll
@@ -855,9 +904,167 @@ __global__ __launch_bounds__(256) void k_mix_tile(
             const int row = __builtin_amdgcn_readlane(d_row, r);
             if (row < 0) continue;                                  // wave-uniform
             float *dst = y + (int64_t)row * ld_y;
+            float o[NE];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) { o[2 * h] = acc[r][h].x; o[2 * h + 1] = acc[r][h].y; }
 #pragma unroll
             for (int q = 0; q < S; ++q)
-                if (ok[q]) stv_nt<VW>(dst + cs[q], acc[r] + q * VW);
+                if (ok[q]) stv_nt<VW>(dst + cs[q], o + q * VW);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// LDS-staged merged-order row tiles (exact and fast; the exact-mode default for clique graphs).
+// Work item = (group, 128-column chunk); a group is a clique (its tiles, niidmix.tile).  The block
+// first stages the chunk of every DISTINCT source row the group reads (its members + gateway rows of
+// other cliques) in LDS — one HBM read per row — then each wave walks one tile's merged position
+// list reading sources from LDS (ds_read_b64, no global-load latency in the loop) into RT packed
+// accumulators per lane (2 columns per lane).  Exact: each row still applies its own entries in its
+// own order with the reference's roundings; a POS_UNIFORM position forms fl(w*x) once.
+// Work order is XCD-aware (the groups of one chunk run back to back on one XCD) so the gateway rows
+// a group stages from other cliques are that XCD's L2 hits.
+constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
+
+template <bool EXACT, int RT, int SV>
+__global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
+    const int32_t *__restrict__ grp_src_rows, const int64_t *__restrict__ sub_ptr,
+    const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
+    const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
+    constexpr int64_t CW = 128;                  // columns per item: 64 lanes x 2
+    constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
+    constexpr int D = 4;                         // positions read together
+    extern __shared__ float lds_tile[];          // [n_src][64] column pairs
+    f2 *stage = reinterpret_cast<f2 *>(lds_tile);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = wave_id();
+    const int n_waves = (int)(blockDim.x >> 6);
+    const int64_t t = blockIdx.x;
+    const int64_t xcd = t & 7, local = t >> 3;
+    const int64_t chunk = (local / n_grp) * 8 + xcd;
+    const int64_t grp = local % n_grp;
+    const int64_t c0 = chunk * CW;
+    if (c0 >= p) return;                         // block-uniform; no barrier reached yet
+    // 1. stage the group's source rows: SV floats per piece, pieces of one row are contiguous
+    {
+        constexpr int PPR = (int)(CW / SV);      // pieces per row
+        const int s0 = grp_src_ptr[grp], ns = grp_src_ptr[grp + 1] - s0;
+        const int total = ns * PPR;
+        float *st = lds_tile;
+        for (int i0 = 0; i0 < total; i0 += 4 * (int)blockDim.x) {
+            float v[4][SV];
+            int at[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + k * (int)blockDim.x + (int)threadIdx.x;
+                const int ii = i < total ? i : total - 1;            // clamped: loads unconditional
+                const int slot = ii / PPR, piece = ii - slot * PPR;
+                const int64_t c = c0 + (int64_t)piece * SV;
+                const int64_t cc = c < p ? c : c0;                  // columns past p: any valid data
+                ldv<SV>(x + (int64_t)grp_src_rows[s0 + slot] * ld_x + cc, v[k]);
+                at[k] = i < total ? slot * (int)CW + piece * SV : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (at[k] >= 0) {
+                    if constexpr (SV == 4)
+                        *reinterpret_cast<float4 *>(st + at[k]) = make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+                    else
+                        *reinterpret_cast<float2 *>(st + at[k]) = make_float2(v[k][0], v[k][1]);
+                }
+        }
+    }
+    __syncthreads();
+    const int64_t col = c0 + 2 * lane;
+    const bool ok = col < p;                     // p even: a lane's pair is all-in or all-out
+    const int tb = grp_tile_ptr[grp], te = grp_tile_ptr[grp + 1];
+    for (int sub = tb + wave; sub < te; sub += n_waves) {
+        const int li = lane < RT ? lane : RT - 1;
+        const int d_row = sub_rows[sub * RT + li];
+        const int d_slot = sub_slot[sub * RT + li];
+        const float d_ws = sub_wself[sub * RT + li];
+        f2 acc[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
+            const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
+            acc[r] = axpy2<EXACT>(ws, xs, xs * 0.f);
+        }
+        const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
+        for (int64_t kb = beg; kb < end; kb += 64) {
+            // 64 positions' (slot, mask, uniform weight) fetched lane-parallel and handed out by
+            // v_readlane: the position loop issues no scalar or global loads (only per-row weights
+            // of a non-uniform position are read from pos_w)
+            const int cnt = (int)(end - kb < 64 ? end - kb : 64);
+            const int lj = lane < cnt ? lane : cnt - 1;
+            const int d_src = pos_slot[kb + lj];
+            const int d_mask = (int)pos_mask[kb + lj];
+            const int d_wu = __float_as_int(pos_w[(kb + lj) * RT]);
+            // LDS reads double-buffered: batch j+D is read while batch j is applied
+            f2 xa[D], xb[D];
+#pragma unroll
+            for (int u = 0; u < D; ++u)
+                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * 64 + lane];
+            for (int j = 0; j < cnt; j += D) {
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    const int jn = j + D + u < cnt ? j + D + u : cnt - 1;
+                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * 64 + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    if (j + u >= cnt) break;
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                    const bool uni = (__builtin_amdgcn_readlane(d_src, j + u) & kPosUniform) != 0;
+                    if (uni) {
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, j + u));
+                        if (EXACT) {
+                            const f2 tp = xa[u] * w;              // one product for the tile
+                            if (m == FULL) {
+#pragma unroll
+                                for (int r = 0; r < RT; ++r) acc[r] = acc[r] + tp;
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < RT; ++r)
+                                    if ((m >> r) & 1u) acc[r] = acc[r] + tp;      // wave-uniform
+                            }
+                        } else if (m == FULL) {
+#pragma unroll
+                            for (int r = 0; r < RT; ++r) acc[r] = axpy2<false>(w, xa[u], acc[r]);
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < RT; ++r)
+                                if ((m >> r) & 1u) acc[r] = axpy2<false>(w, xa[u], acc[r]);
+                        }
+                    } else {
+                        const float *wp = pos_w + (kb + j + u) * RT;
+#pragma unroll
+                        for (int r = 0; r < RT; ++r)
+                            if ((m >> r) & 1u) acc[r] = axpy2<EXACT>(wp[r], xa[u], acc[r]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < D; ++u) xa[u] = xb[u];
+            }
+        }
+        // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc)
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+            const int row = __builtin_amdgcn_readlane(d_row, r);
+            if (row < 0) continue;                                  // wave-uniform
+            f2 o = acc[r];
+            if (!avg_only) {
+                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
+                o = xs * 0.f + acc[r];
+            }
+            if (ok) {
+                float *dst = y + (int64_t)row * ld_y + col;
+                __builtin_nontemporal_store(o.x, dst);
+                __builtin_nontemporal_store(o.y, dst + 1);
+            }
         }
     }
 }
@@ -1212,6 +1419,54 @@ int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
 #undef NIIDMIX_TILE_V
 #undef NIIDMIX_TILEK
     return check_launch("k_mix_tile");
+}
+
+int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                             const niidmix_tile_lds_plan *plan, int mode, void *stream) {
+    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (p < 0 || plan->n_grp < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (plan->rt != 8 && plan->rt != 16 && plan->rt != 32)
+        return set_error(NIIDMIX_EUNSUPPORTED, "tile of %d rows (8, 16 or 32 supported)", plan->rt);
+    if (plan->n_grp == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !plan->grp_tile_ptr || !plan->grp_src_ptr || !plan->grp_src_rows ||
+        !plan->sub_ptr || !plan->sub_rows || !plan->sub_slot || !plan->sub_wself ||
+        !plan->pos_slot || !plan->pos_mask || !plan->pos_w)
+        return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (plan->max_src < 1 || plan->max_src > 256)
+        return set_error(NIIDMIX_EUNSUPPORTED, "group with %d source rows (1..256 supported)", plan->max_src);
+    const int max_waves = tile_lds_max_waves(plan->rt);
+    if (plan->max_tiles < 1 || plan->max_tiles > max_waves)
+        return set_error(NIIDMIX_EUNSUPPORTED, "group with %d tiles of %d rows (1..%d supported)",
+                         plan->max_tiles, plan->rt, max_waves);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    if (p % 2 || ld_x % 2 || ld_y % 2 || (align & 7))
+        return set_error(NIIDMIX_EUNSUPPORTED, "LDS tile kernel needs even p, ld and 8-B aligned slabs");
+    const int sv = (p % 4 == 0 && ld_x % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 4 : 2;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n_chunks = (p + 127) / 128;
+    const int64_t n_items = (int64_t)plan->n_grp * ((n_chunks + 7) / 8) * 8;
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
+    const size_t lds = (size_t)plan->max_src * 128 * sizeof(float);
+    const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
+#define NIIDMIX_TLDS(E, R, V) do { \
+        auto kfn = k_mix_tile_lds<E, R, V>; \
+        if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+            return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \
+    } while (0)
+#define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
+#define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)
+    if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_TLDS_R(true); else NIIDMIX_TLDS_R(false);
+#undef NIIDMIX_TLDS_R
+#undef NIIDMIX_TLDS_V
+#undef NIIDMIX_TLDS
+    return check_launch("k_mix_tile_lds");
 }
 
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,

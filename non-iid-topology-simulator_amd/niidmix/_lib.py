@@ -41,6 +41,14 @@ class TilePlanC(ctypes.Structure):
                 ("sub_wself", _vp), ("pos_src", _vp), ("pos_mask", _vp), ("pos_w", _vp)]
 
 
+class TileLdsPlanC(ctypes.Structure):
+    """Mirror of struct niidmix_tile_lds_plan (include/niidmix.h)."""
+    _fields_ = [("n_sub", _i64), ("rt", _i32), ("n_grp", _i32), ("max_src", _i32), ("max_tiles", _i32),
+                ("sub_ptr", _vp), ("sub_rows", _vp), ("sub_slot", _vp), ("sub_wself", _vp),
+                ("pos_slot", _vp), ("pos_mask", _vp), ("pos_w", _vp), ("grp_tile_ptr", _vp),
+                ("grp_src_ptr", _vp), ("grp_src_rows", _vp)]
+
+
 # every symbol include/niidmix.h declares, with its ctypes signature
 SIGNATURES = {
     "niidmix_abi_version": (ctypes.c_int, []),
@@ -53,6 +61,8 @@ SIGNATURES = {
                                               ctypes.POINTER(StagedPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                             ctypes.POINTER(TilePlanC), ctypes.c_int, _vp]),
+    "niidmix_mix_tile_lds_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+                                                ctypes.POINTER(TileLdsPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp,

@@ -4,6 +4,8 @@ Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
   mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, out,
              max_clique, max_clique_res)            k_mix_clique_wave (fast, HBM-bound)
+  mix_tile_lds(x, <tile lds plan tensors>, out, rt, max_src, max_tiles, mode)
+                                                    k_mix_tile_lds (exact default, LDS-staged)
   mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
   grad_segment_mean(g, seg_ptr, seg_row, out)       k_grad_segment_mean (clique gradient mean)
@@ -21,7 +23,7 @@ import torch
 from . import _lib
 from .factor import build_clique_plan
 from .staged import build_staged_plan
-from .tile import build_tile_plan
+from .tile import LDS_MAX_WAVES, build_tile_lds_plan, build_tile_plan
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -174,6 +176,39 @@ def mix_tile(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
     _lib.check(rc, "niidmix::mix_tile")
 
 
+@torch.library.custom_op("niidmix::mix_tile_lds", mutates_args=("out",))
+def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
+                 sub_slot: torch.Tensor, sub_wself: torch.Tensor, pos_slot: torch.Tensor,
+                 pos_mask: torch.Tensor, pos_w: torch.Tensor, grp_tile_ptr: torch.Tensor,
+                 grp_src_ptr: torch.Tensor, grp_src_rows: torch.Tensor, out: torch.Tensor, rt: int,
+                 max_src: int, max_tiles: int, mode: int) -> None:
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    dev = x.device
+    t = sub_ptr.numel() - 1
+    g = grp_tile_ptr.numel() - 1
+    _vec("sub_ptr", sub_ptr, torch.int64, dev)
+    _vec("sub_rows", sub_rows, torch.int32, dev, t * rt)
+    _vec("sub_slot", sub_slot, torch.int32, dev, t * rt)
+    _vec("sub_wself", sub_wself, torch.float32, dev, t * rt)
+    _vec("pos_slot", pos_slot, torch.int32, dev)
+    _vec("pos_mask", pos_mask, torch.int32, dev, pos_slot.numel())      # uint32 bits
+    _vec("pos_w", pos_w, torch.float32, dev, pos_slot.numel() * rt)
+    _vec("grp_tile_ptr", grp_tile_ptr, torch.int32, dev)
+    _vec("grp_src_ptr", grp_src_ptr, torch.int32, dev, g + 1)
+    _vec("grp_src_rows", grp_src_rows, torch.int32, dev)
+    _no_overlap(x, out)
+    some = sub_ptr.data_ptr()
+    plan = _lib.TileLdsPlanC(t, int(rt), g, int(max_src), int(max_tiles), sub_ptr.data_ptr(),
+                             sub_rows.data_ptr(), sub_slot.data_ptr(), sub_wself.data_ptr(),
+                             pos_slot.data_ptr() or some, pos_mask.data_ptr() or some,
+                             pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
+                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr())
+    rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
+                                           x.shape[1], ctypes.byref(plan), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_tile_lds")
+
+
 @torch.library.custom_op("niidmix::mix_dense", mutates_args=("out",))
 def mix_dense(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
     _slab("x", x)
@@ -281,6 +316,29 @@ class Mixer:
             self.t_pos_src = torch.from_numpy(tp.pos_src).to(dev)
             self.t_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
             self.t_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+        # LDS-staged tiles (exact mode's default where they build: every clique's distinct source
+        # rows fit the LDS stage); NIIDMIX_TILE_LDS_RT=8|16|32 picks the tile height
+        self.tlds, self.tlds_reason = (None, "average degree < 8")
+        if csr.nnz >= 9 * max(csr.n, 1):
+            rt = int(os.environ.get("NIIDMIX_TILE_LDS_RT", "16"))
+            grp = cliques
+            if not grp:
+                span = rt * LDS_MAX_WAVES.get(rt, 1)
+                grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
+            self.tlds, self.tlds_reason = build_tile_lds_plan(csr, grp, rt)
+        if self.tlds is not None:
+            lp = self.tlds
+            tp = lp.tile
+            self.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+            self.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+            self.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
+            self.l_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+            self.l_pos_slot = torch.from_numpy(lp.pos_slot).to(dev)
+            self.l_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+            self.l_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+            self.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
+            self.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
+            self.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
@@ -290,6 +348,8 @@ class Mixer:
             # measured on the 1000-node d-cliques round (P = 2^20): merged-order row tiles of 8
             # rows 5.9 ms, CSR gather 23.1 ms, LDS-staged 23.9 ms; the tile plan exists only for
             # graphs with average degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
+            if self.tlds is not None and (x is None or _lds_ok(x)) and (out is None or _lds_ok(out)):
+                return "tile-lds-exact"
             return "tile-exact" if self.tile is not None else "csr-exact"
         if self.plan is not None and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
@@ -316,6 +376,13 @@ class Mixer:
             mix_tile(x, self.t_sub_ptr, self.t_sub_rows, self.t_sub_wself, self.t_pos_src,
                      self.t_pos_mask, self.t_pos_w, out, self.tile.rt,
                      EXACT if k == "tile-exact" else FAST)
+        elif k in ("tile-lds-exact", "tile-lds-fast"):
+            _req(self.tlds is not None, f"no LDS tile plan: {self.tlds_reason}")
+            lp = self.tlds
+            mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
+                         self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
+                         self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,
+                         lp.max_tiles, EXACT if k == "tile-lds-exact" else FAST)
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
@@ -333,6 +400,11 @@ class Mixer:
 def _clique_ok(x):
     """k_mix_clique streams float4 columns: p and ld multiples of 4, 16-B aligned base."""
     return x.shape[1] % 4 == 0 and _ld(x) % 4 == 0 and x.data_ptr() % 16 == 0
+
+
+def _lds_ok(x):
+    """k_mix_tile_lds reads column pairs: even p and ld, 8-B aligned base."""
+    return x.shape[1] % 2 == 0 and _ld(x) % 2 == 0 and x.data_ptr() % 8 == 0
 
 
 def csr_from_numpy(row_ptr, col, val):

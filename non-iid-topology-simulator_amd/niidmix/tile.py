@@ -17,6 +17,7 @@ from dataclasses import dataclass
 import numpy as np
 
 TILE_ROWS = (8, 16, 32)
+POS_UNIFORM = 1 << 30          # pos_src flag: every tile row's weight at this position is equal
 
 
 @dataclass
@@ -25,10 +26,11 @@ class TilePlan:
     sub_ptr: np.ndarray     # int64 [T+1] offsets into the position arrays
     sub_rows: np.ndarray    # int32 [T*rt], -1 = unused slot
     sub_wself: np.ndarray   # fp32 [T*rt]
-    pos_src: np.ndarray     # int32 [L]
+    pos_src: np.ndarray     # int32 [L] source row | POS_UNIFORM
     pos_mask: np.ndarray    # uint32 [L]
     pos_w: np.ndarray       # fp32 [L*rt]
     nnz: int                # off-diagonal entries covered
+    grp_tile_ptr: np.ndarray = None   # int32 [G+1]: tiles of each input group
 
     @property
     def n_sub(self):
@@ -54,7 +56,8 @@ class TilePlan:
                 lst = [(row, np.float32(self.sub_wself[t * self.rt + r]))]
                 for k in range(b, e):
                     if (int(self.pos_mask[k]) >> r) & 1:
-                        lst.append((int(self.pos_src[k]), np.float32(self.pos_w[k * self.rt + r])))
+                        lst.append((int(self.pos_src[k]) & (POS_UNIFORM - 1),
+                                    np.float32(self.pos_w[k * self.rt + r])))
                 out[row] = lst
         return out
 
@@ -134,9 +137,42 @@ def _split(rows, rt):
     return parts
 
 
+def _class_tiles(group, rp, val, rt):
+    """Tiles of a row group: rows ordered by degree — under Metropolis-Hastings the weight
+    W[j, i] = 1/(max(d_i, d_j) + 1) a source j carries into row i depends on i only through d_i —
+    and each degree class cut on its own, so a source's weight is the same across a tile's rows
+    (POS_UNIFORM; checked on the actual values) — e.g. the gateway rows of a D-Clique form their own
+    tile.  Classes of fewer than max(2, rt/2) rows are merged into a neighbouring class (their
+    positions are then weighted per row)."""
+    key = lambda r: int(rp[r + 1] - rp[r])
+    rows = sorted(group, key=key)
+    runs = []
+    for r in rows:
+        if runs and key(runs[-1][-1]) == key(r):
+            runs[-1].append(r)
+        else:
+            runs.append([r])
+    small = max(2, rt // 2)                 # a class this small would waste a mostly empty tile
+    merged = []
+    for run in runs:
+        if merged and len(merged[-1]) < small:
+            merged[-1].extend(run)
+        else:
+            merged.append(list(run))
+    if len(merged) > 1 and len(merged[-1]) < small:
+        merged[-2].extend(merged.pop())
+    return [part for run in merged for part in _split(run, rt)]
+
+
 def build_tile_plan(csr, groups=None, rt=16):
     """(plan, None) or (None, reason).  groups: row lists (e.g. the cliques) cut into tiles of <= rt
-    rows; None -> consecutive rows.  Every CSR row must belong to exactly one group."""
+    rows; None -> consecutive rows.  Every CSR row must belong to exactly one group.
+
+    Inside a group rows are ordered by their self weight, then degree (stable) before the cut, so a
+    tile holds rows of one Metropolis-Hastings degree class (D-Cliques: the gateway rows together):
+    the weights a source carries into a tile's rows are then equal, the position is flagged
+    POS_UNIFORM and the exact kernel forms each product once for the whole tile (its weight is
+    replicated into every slot of pos_w)."""
     if rt not in TILE_ROWS:
         return None, f"rt={rt} not in {TILE_ROWS}"
     n = csr.n
@@ -149,20 +185,27 @@ def build_tile_plan(csr, groups=None, rt=16):
     full = (1 << rt) - 1
     sub_ptr, sub_rows, sub_wself = [0], [], []
     pos_src, pos_mask, pos_w = [], [], []
+    grp_tile_ptr = [0]
     for g in groups:
-        for part in _split(list(g), rt):
+        for part in _class_tiles(g, rp, val, rt):
             lists = [(col[rp[r] + 1:rp[r + 1]], val[rp[r] + 1:rp[r + 1]]) for r in part]
             pad = full & ~((1 << len(part)) - 1)
             for c, mask, ws in _merge(lists):
                 w = np.zeros(rt, np.float32)
-                for r, v in ws.items():
-                    w[r] = v
+                vals = np.asarray(list(ws.values()), np.float32)
+                if len(vals) and np.all(vals.view(np.uint32) == vals[:1].view(np.uint32)):
+                    w[:] = vals[0]
+                    c = int(c) | POS_UNIFORM
+                else:
+                    for r, v in ws.items():
+                        w[r] = v
                 pos_src.append(c)
                 pos_mask.append(mask | pad)
                 pos_w.append(w)
             sub_ptr.append(len(pos_src))
             sub_rows.extend(list(part) + [-1] * (rt - len(part)))
             sub_wself.extend([val[rp[r]] for r in part] + [0.0] * (rt - len(part)))
+        grp_tile_ptr.append(len(sub_ptr) - 1)
     L = len(pos_src)
     return TilePlan(
         rt=rt, sub_ptr=np.asarray(sub_ptr, np.int64),
@@ -170,7 +213,70 @@ def build_tile_plan(csr, groups=None, rt=16):
         pos_src=np.asarray(pos_src, np.int32).reshape(L),
         pos_mask=np.asarray(pos_mask, np.uint64).astype(np.uint32).reshape(L),
         pos_w=(np.stack(pos_w) if L else np.zeros((0, rt), np.float32)).reshape(L * rt),
-        nnz=int(csr.nnz - csr.n)), None
+        nnz=int(csr.nnz - csr.n), grp_tile_ptr=np.asarray(grp_tile_ptr, np.int32)), None
+
+
+LDS_MAX_SRC = 256
+LDS_MAX_WAVES = {8: 16, 16: 8, 32: 4}
+
+
+@dataclass
+class TileLdsPlan:
+    """A TilePlan regrouped for k_mix_tile_lds: each group (clique) stages its distinct source rows
+    in LDS; positions and tile rows refer to LDS slots."""
+    tile: TilePlan
+    pos_slot: np.ndarray      # int32 [L] slot | POS_UNIFORM
+    sub_slot: np.ndarray      # int32 [T*rt]
+    grp_tile_ptr: np.ndarray  # int32 [G+1]
+    grp_src_ptr: np.ndarray   # int32 [G+1]
+    grp_src_rows: np.ndarray  # int32 [sum of group source counts]
+    max_src: int
+    max_tiles: int
+
+    @property
+    def n_grp(self):
+        return len(self.grp_tile_ptr) - 1
+
+
+def build_tile_lds_plan(csr, groups=None, rt=8):
+    """(plan, None) or (None, reason): build_tile_plan over `groups`, then per group the sorted list
+    of distinct source rows (every row its tiles read, self rows included) and the slot indices."""
+    if rt not in LDS_MAX_WAVES:
+        return None, f"rt={rt} not in {tuple(LDS_MAX_WAVES)}"
+    tp, why = build_tile_plan(csr, groups, rt)
+    if tp is None:
+        return None, why
+    row_mask = POS_UNIFORM - 1
+    gtp = tp.grp_tile_ptr
+    pos_slot = np.empty_like(tp.pos_src)
+    sub_slot = np.zeros_like(tp.sub_rows)
+    src_ptr, src_rows = [0], []
+    max_src = max_tiles = 0
+    for gi in range(len(gtp) - 1):
+        t0, t1 = int(gtp[gi]), int(gtp[gi + 1])
+        p0, p1 = int(tp.sub_ptr[t0]), int(tp.sub_ptr[t1])
+        rows = tp.sub_rows[t0 * rt:t1 * rt]
+        srcs = np.unique(np.concatenate([tp.pos_src[p0:p1] & row_mask, rows[rows >= 0]]))
+        if len(srcs) > LDS_MAX_SRC:
+            return None, f"group {gi} reads {len(srcs)} distinct rows (> {LDS_MAX_SRC})"
+        if t1 - t0 > LDS_MAX_WAVES[rt]:
+            return None, f"group {gi} has {t1 - t0} tiles of {rt} rows (> {LDS_MAX_WAVES[rt]})"
+        slot_of = {int(r): i for i, r in enumerate(srcs)}
+        for k in range(p0, p1):
+            v = int(tp.pos_src[k])
+            pos_slot[k] = slot_of[v & row_mask] | (v & POS_UNIFORM)
+        for k in range(t0 * rt, t1 * rt):
+            r = int(tp.sub_rows[k])
+            sub_slot[k] = slot_of[r] if r >= 0 else 0
+        src_rows.extend(int(r) for r in srcs)
+        src_ptr.append(len(src_rows))
+        max_src = max(max_src, len(srcs))
+        max_tiles = max(max_tiles, t1 - t0)
+    return TileLdsPlan(tile=tp, pos_slot=pos_slot, sub_slot=sub_slot,
+                       grp_tile_ptr=np.asarray(gtp, np.int32),
+                       grp_src_ptr=np.asarray(src_ptr, np.int32),
+                       grp_src_rows=np.asarray(src_rows, np.int32),
+                       max_src=max(max_src, 1), max_tiles=max(max_tiles, 1)), None
 
 
 def apply_np(plan, x, exact=True, average_only=False):

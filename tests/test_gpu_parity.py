@@ -96,11 +96,78 @@ def test_tile_exact_heights_bitwise(name, rt, gpu, oracle_mod):
     assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref), (name, rt)
 
 
+def _tile_lds_mixer(g, dev, rt):
+    """A Mixer with an LDS tile plan of height rt for any golden topology (tests only): cliques
+    as groups where the fixture has them, else consecutive row blocks."""
+    from niidmix import tile
+    m = _mixer(g, dev)
+    cl = g.get("cliques")
+    if not cl:
+        span = rt * tile.LDS_MAX_WAVES[rt]
+        cl = [list(range(s, min(s + span, m.n))) for s in range(0, m.n, span)]
+    lp, why = tile.build_tile_lds_plan(m.csr, cl, rt)
+    if lp is None:
+        pytest.skip(why)
+    tp = lp.tile
+    m.tlds = lp
+    m.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+    m.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+    m.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
+    m.l_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+    m.l_pos_slot = torch.from_numpy(lp.pos_slot).to(dev)
+    m.l_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+    m.l_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+    m.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
+    m.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
+    m.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
+    return m
+
+
+@pytest.mark.parametrize("rt", [8, 16, 32])
+@pytest.mark.parametrize("name", golden_cases())
+def test_tile_lds_bitwise(name, rt, gpu, oracle_mod):
+    """The LDS-staged tile kernel (exact) is bit-identical to the reference on every golden case
+    and tile height, average-only flag included; fast mode meets the 1e-5 condition-aware bound."""
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    m = _tile_lds_mixer(g, gpu, rt)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-lds-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"]), (name, rt)
+    ops = _ops()
+    lp = m.tlds
+    out = torch.empty_like(x)
+    ops.mix_tile_lds(x, m.l_sub_ptr, m.l_sub_rows, m.l_sub_slot, m.l_sub_wself, m.l_pos_slot,
+                     m.l_pos_mask, m.l_pos_w, m.l_grp_tile_ptr, m.l_grp_src_ptr, m.l_grp_src_rows,
+                     out, rt, lp.max_src, lp.max_tiles, ops.EXACT | ops.AVERAGE_ONLY)
+    ref = oracle_mod.mix_exact_c(g["x"], g["row_ptr"], g["col"], g["val"], average_only=True)
+    assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref), (name, rt)
+    if np.all(np.isfinite(g["x"])):
+        yf = m(x, kernel="tile-lds-fast").cpu().numpy()
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        ok, worst = oracle_mod.check_tolerance(yf, g["y"], bound, rtol=RTOL)
+        assert ok, (name, rt, worst)
+
+
+def test_tile_lds_strided_window(gpu, oracle_mod):
+    """A column window of a wider slab (ld > p, p not a multiple of 128 or 4)."""
+    g = load_golden("dcliques1000_fc_p64")
+    m = _tile_lds_mixer(g, gpu, 16)
+    gen = torch.Generator().manual_seed(3)
+    full = torch.randn(1000, 1000, generator=gen)
+    x = full.to(gpu)[:, 2:2 + 522]
+    out = torch.zeros((1000, 1024), device=gpu)[:, 6:6 + 522]
+    m(x, out=out, kernel="tile-lds-exact")
+    ref = oracle_mod.mix_exact_c(full.numpy(), g["row_ptr"], g["col"], g["val"], cols=(2, 524))
+    assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref[:, 2:524])
+
+
 def test_auto_kernel_choice(gpu):
     g = load_golden("dcliques1000_fc_p64")
     m = _mixer(g, gpu)
     assert m.kernel_for("fast") == "clique"
-    assert m.kernel_for("exact") == "tile-exact"
+    assert m.kernel_for("exact") == "tile-lds-exact"
     g = load_golden("fc64_p33")
     assert _mixer(g, gpu).kernel_for("fast") == "clique"      # MH fully-connected = one clique
     ops = _ops()

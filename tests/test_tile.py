@@ -81,3 +81,45 @@ def test_bad_inputs():
     g = load_golden("ring100_p257")
     assert tile.build_tile_plan(_csr(g), None, 12)[0] is None
     assert tile.build_tile_plan(_csr(g), [[0, 1]], 16)[0] is None     # not a partition
+
+
+@pytest.mark.parametrize("rt", [8, 16, 32])
+@pytest.mark.parametrize("name", ["dcliques1000_fc_p64", "dcliques1000_smallworld_p16",
+                                  "dcliques200_fractal_rm5_p40", "dcliques300_fc_p37"])
+def test_lds_plan_slots(name, rt):
+    """LDS plan: every position / tile row slot names, in its group's staged list, the row the
+    global tile plan names; lists are distinct and within the LDS budget; the uniform flag is kept
+    and holds (all rt weights of a flagged position equal)."""
+    from niidmix import tile
+    g = load_golden(name)
+    csr = _csr(g).validate()
+    lp, why = tile.build_tile_lds_plan(csr, g["cliques"], rt)
+    if lp is None:
+        pytest.skip(why)
+    tp = lp.tile
+    mask = tile.POS_UNIFORM - 1
+    assert lp.max_src <= tile.LDS_MAX_SRC and lp.max_tiles <= tile.LDS_MAX_WAVES[rt]
+    for gi in range(lp.n_grp):
+        srcs = lp.grp_src_rows[lp.grp_src_ptr[gi]:lp.grp_src_ptr[gi + 1]]
+        assert len(np.unique(srcs)) == len(srcs)
+        t0, t1 = lp.grp_tile_ptr[gi], lp.grp_tile_ptr[gi + 1]
+        for k in range(tp.sub_ptr[t0], tp.sub_ptr[t1]):
+            assert srcs[lp.pos_slot[k] & mask] == (tp.pos_src[k] & mask)
+            assert (lp.pos_slot[k] & tile.POS_UNIFORM) == (tp.pos_src[k] & tile.POS_UNIFORM)
+            if tp.pos_src[k] & tile.POS_UNIFORM:
+                w = tp.pos_w[k * rt:(k + 1) * rt]
+                assert np.all(w.view(np.uint32) == w[0].view(np.uint32))
+        for k in range(t0 * rt, t1 * rt):
+            if tp.sub_rows[k] >= 0:
+                assert srcs[lp.sub_slot[k]] == tp.sub_rows[k]
+
+
+def test_uniform_positions_dominate_dcliques():
+    """Degree-class ordering inside a clique makes almost every position uniform-weight on the
+    headline topology (the exact kernel then forms one product per position)."""
+    from niidmix import tile
+    g = load_golden("dcliques1000_fc_p64")
+    csr = _csr(g).validate()
+    tp, _ = tile.build_tile_plan(csr, g["cliques"], 16)
+    frac = np.mean((tp.pos_src & tile.POS_UNIFORM) != 0)
+    assert frac > 0.95, frac

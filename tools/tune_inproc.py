@@ -42,22 +42,31 @@ def main():
         variants.append((name, envd, kernel))
     mixers = {}
 
+    plan_env = ("NIIDMIX_TILE_RT", "NIIDMIX_TILE_LDS_RT")
+
     def mixer_for(envd):
-        rt = envd.get("NIIDMIX_TILE_RT")
-        if rt is None:
+        key = tuple(envd.get(k) for k in plan_env)
+        if all(v is None for v in key):
             return m
-        if rt not in mixers:
-            saved = os.environ.get("NIIDMIX_TILE_RT")
-            os.environ["NIIDMIX_TILE_RT"] = rt
-            mixers[rt] = ops.Mixer(csr=csr, cliques=cl, device=dev)
-            if saved is None:
-                os.environ.pop("NIIDMIX_TILE_RT")
-            else:
-                os.environ["NIIDMIX_TILE_RT"] = saved
-            t = mixers[rt].tile
-            if t is not None:
-                print(f"tile rt={rt}: {t.n_sub} tiles, {t.n_pos} positions, density {t.density:.3f}")
-        return mixers[rt]
+        if key not in mixers:
+            saved = {k: os.environ.get(k) for k in plan_env}
+            for k in plan_env:
+                if envd.get(k) is not None:
+                    os.environ[k] = envd[k]
+            mixers[key] = ops.Mixer(csr=csr, cliques=cl, device=dev)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            t = mixers[key].tile
+            if t is not None and key[0] is not None:
+                print(f"tile rt={key[0]}: {t.n_sub} tiles, {t.n_pos} positions, density {t.density:.3f}")
+            t = mixers[key].tlds
+            if t is not None and key[1] is not None:
+                print(f"lds tile rt={key[1]}: {t.tile.n_sub} tiles, {t.tile.n_pos} positions, "
+                      f"density {t.tile.density:.3f}, max_src {t.max_src}, max_tiles {t.max_tiles}")
+        return mixers[key]
 
     res = {n: [] for n, _, _ in variants}
     res["copy"] = []
@@ -81,7 +90,7 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-        res["copy"].append(2 * x.numel() * 4 / bench.stream_copy_probe(x, y) / 1e9 * 1e3)
+        res["copy"].append(2 * x.numel() * 4 / (bench.stream_copy_probe(x.numel(), dev) * 1e9) * 1e3)
     alg = 2 * csr.n * p * 4
     print(f"config {a.config} N={csr.n} P={p}  ({desc})")
     for name, t in res.items():
