@@ -104,6 +104,10 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *   coef         [n_members * (1 + n_groups)] fp32: a_m, then c_{m,0..n_groups-1}
  *   res_ptr      [n_members+1] int32 offsets into res_col/res_val (residual sparse terms)
  *   res_col      [n_res] int32 input rows, res_val [n_res] fp32
+ *   res_member   [n_res] int32 index, within its clique, of the member each residual entry belongs
+ *                to (the register tile fetches a clique's residual entries lane-parallel together
+ *                with the member descriptors, so the gateway-row gathers issue right behind the
+ *                member-row loads)
  *   max_clique   largest clique size: <= 256 selects a register tile (one HBM read per
  *                parameter); larger cliques (e.g. fully-connected = one clique) use a two-pass
  *                kernel whose second read is served from L2 / Infinity Cache
@@ -122,6 +126,7 @@ typedef struct niidmix_clique_plan {
     const int32_t *res_ptr;
     const int32_t *res_col;
     const float *res_val;
+    const int32_t *res_member;
 } niidmix_clique_plan;
 
 int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,

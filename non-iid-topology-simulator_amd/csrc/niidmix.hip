@@ -213,15 +213,18 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
 // Work order is XCD-aware (the cliques of one chunk run back to back on one XCD) so the residual
 // rows a gateway gathers from another clique are normally still in that XCD's L2.
 template <int G, int RW>
-struct CliqueDesc {        // one work item's member descriptors, lane-parallel (lane r = slot r)
-    int32_t m0, M;         // wave-uniform
-    int row, grp, rb, re;  // per lane
+struct CliqueDesc {        // one work item's descriptors, lane-parallel
+    int32_t m0, M;         // wave-uniform: first member, members (0 past p)
+    int32_t cr0, ncr;      // wave-uniform: the clique's residual entries [cr0, cr0 + ncr)
+    int row, grp;          // lane r < RPW: the wave's r-th member (slot r)
     float cf[1 + G];
-    int nres;              // wave-uniform: residual entries of this wave's members
-    int rsrc, rslot;       // lane j < RW: j-th residual entry of this wave (source row, member slot,
-    float rw;              //   weight)
+    int rsrc, rk;          // lane j < min(ncr, RW): the clique's j-th residual entry (source row,
+    float rw;              //   member index within the clique, weight); rk = -1 past the list
 };
 
+// All descriptors of a work item in ONE dependent step after the clique offsets: the members'
+// (row, group, coefficients) and the clique's residual entries (gateway edges), so the residual
+// rows can be gathered right behind the member rows instead of one memory round trip later.
 template <int WAVES, int RPW, int G, int RW, int64_t CW>
 __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t, int32_t n_cliques,
                                                  int64_t p, int wave, int lane,
@@ -229,49 +232,35 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
                                                  const int32_t *__restrict__ member_row,
                                                  const int32_t *__restrict__ member_group,
                                                  const float *__restrict__ coef,
-                                                 const int32_t *__restrict__ res_ptr) {
+                                                 const int32_t *__restrict__ res_ptr,
+                                                 const int32_t *__restrict__ res_col,
+                                                 const float *__restrict__ res_val,
+                                                 const int32_t *__restrict__ res_member) {
     const int64_t local = t >> 3;
     const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
     const int32_t cq = (int32_t)(local % n_cliques);
+    const bool valid = chunk * CW < p;
     d.m0 = clique_ptr[cq];
-    d.M = chunk * CW < p ? clique_ptr[cq + 1] - d.m0 : 0;
+    const int32_t m1 = clique_ptr[cq + 1];
+    d.M = valid ? m1 - d.m0 : 0;
+    d.cr0 = res_ptr[d.m0];
+    d.ncr = valid ? res_ptr[m1] - d.cr0 : 0;
     const int kd = wave + WAVES * lane;
-    d.row = 0; d.grp = 0; d.rb = 0; d.re = 0;
+    d.row = 0; d.grp = 0;
 #pragma unroll
     for (int g = 0; g <= G; ++g) d.cf[g] = 0.f;
     if (lane < RPW && kd < d.M) {
         const int32_t m = d.m0 + kd;
         d.row = member_row[m];
         d.grp = member_group[m];
-        d.rb = res_ptr[m];
-        d.re = res_ptr[m + 1];
 #pragma unroll
         for (int g = 0; g <= G; ++g) d.cf[g] = coef[(int64_t)m * (1 + G) + g];
     }
-}
-
-// Second descriptor step, issued AFTER the member-row loads so its latency hides under them: lane j
-// of the wave takes the wave's j-th residual entry (members in slot order, each member's entries in
-// res order) — its source row, weight and the member slot it belongs to.
-template <int RPW, int G, int RW>
-__device__ __forceinline__ void load_res_desc(CliqueDesc<G, RW> &d, int lane,
-                                              const int32_t *__restrict__ res_col,
-                                              const float *__restrict__ res_val) {
-    int pre = 0, q_j = -1, slot = 0;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-        const int rb = __builtin_amdgcn_readlane(d.rb, r);
-        const int cnt = __builtin_amdgcn_readlane(d.re, r) - rb;
-        if (lane >= pre && lane < pre + cnt) { q_j = rb + lane - pre; slot = r; }
-        pre += cnt;
-    }
-    d.nres = pre;
-    d.rslot = slot;
-    d.rsrc = __builtin_amdgcn_readlane(d.row, 0);
-    d.rw = 0.f;
-    if (RW > 0 && lane < RW && q_j >= 0) {
-        d.rsrc = res_col[q_j];
-        d.rw = res_val[q_j];
+    d.rsrc = 0; d.rk = -1; d.rw = 0.f;
+    if (RW > 0 && lane < RW && lane < d.ncr) {
+        d.rsrc = res_col[d.cr0 + lane];
+        d.rk = res_member[d.cr0 + lane];
+        d.rw = res_val[d.cr0 + lane];
     }
 }
 
@@ -289,11 +278,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
-    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val,
+    const int32_t *__restrict__ res_member, int64_t n_items) {
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
     static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
-    constexpr int RU = 2;                     // residual rows gathered per batch
+    // timing-only ablations (WRONG results; tools/tune_inproc.py): 4 = skip residual gathers,
+    // 8 = skip the cross-wave LDS reduction (per-wave group sums only, no barriers)
+    constexpr bool NO_RES = (FL & 4) != 0, NO_RED = (FL & 8) != 0;
+    constexpr int RQ = 2;                     // residual rows per wave held in registers
     constexpr int64_t CW = 64 * V;            // columns per work item
     __shared__ float red[G][WAVES][kWave * V];
     __shared__ float tot[G][kWave * V];
@@ -303,7 +296,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     if (t >= n_items) return;
     CliqueDesc<G, RW> d;
     load_clique_desc<WAVES, RPW, G, RW, CW>(d, t, n_cliques, p, wave, lane, clique_ptr, member_row,
-                                            member_group, coef, res_ptr);
+                                            member_group, coef, res_ptr, res_col, res_val,
+                                            res_member);
     const int64_t local = t >> 3;
     const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
     const bool act = chunk * CW + V * lane < p;
@@ -326,7 +320,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
             }
         }
     }
-    load_res_desc<RPW, G, RW>(d, lane, res_col, res_val);
+    // 1b. residual rows of this wave's members (clique entries whose member index k has
+    //     k % WAVES == wave), issued right behind the member rows: up to RQ in registers, the
+    //     rest (rare) gathered one by one in step 3.  Not non-temporal: a gateway row is another
+    //     clique's member, read again by that clique's block (L2 hit).
+    const int ncr = NO_RES ? 0 : d.ncr;
+    const int nl = ncr < RW ? ncr : RW;
+    uint64_t mine = __ballot(lane < nl && d.rk >= 0 && d.rk % WAVES == wave);
+    float xr[RQ][V];
+    int jq[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+        jq[q] = mine ? __builtin_ctzll(mine) : -1;
+        mine &= mine - 1;
+        const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jq[q] >= 0 ? jq[q] : 0);
+#pragma unroll
+        for (int e = 0; e < V; ++e) xr[q][e] = 0.f;
+        if (act && jq[q] >= 0) ldv<V>(xc + row * ld_x + lo, xr[q]);
+    }
     // 2. per-wave partial group sums -> LDS
     {
         float s[G][V];
@@ -354,64 +365,62 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     }
     // 3. own term and residual terms (gateway edges) in place, BEFORE any store: v[r] := a_r x_r
     //    + sum_res w x_src.  On CDNA vmcnt counts stores too, so a gather issued after a store
-    //    would make the gather's wait drain that store from HBM first.  The wave's first RW
-    //    entries come lane-parallel and are gathered RU rows at a time (unconditional, clamped);
-    //    entries beyond RW (a wave with more than RW residual terms) take a per-entry loop.
+    //    would make the gather's wait drain that store from HBM first.
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
         const float af = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.cf[0]), r));
 #pragma unroll
         for (int e = 0; e < V; ++e) v[r][e] *= af;
     }
-    const int nres = d.nres;
-    const int npre = nres < RW ? nres : RW;
-    for (int j0 = 0; j0 < npre; j0 += RU) {
-        float xr[RU][V];
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            const int jj = j0 + u < npre ? j0 + u : npre - 1;
-            const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jj);
+    for (int q = 0; q < RQ; ++q) {
+        if (jq[q] < 0) break;                                           // wave-uniform
+        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), jq[q]));
+        const int slot = __builtin_amdgcn_readlane(d.rk, jq[q]) / WAVES;
 #pragma unroll
-            for (int e = 0; e < V; ++e) xr[u][e] = 0.f;
-            if (act) ldv<V>(xc + row * ld_x + lo, xr[u]);
-        }
+        for (int r = 0; r < RPW; ++r)
+            if (slot == r) {
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            if (j0 + u >= npre) break;
-            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j0 + u));
-            const int slot = __builtin_amdgcn_readlane(d.rslot, j0 + u);
-#pragma unroll
-            for (int r = 0; r < RPW; ++r)
-                if (slot == r) {
-#pragma unroll
-                    for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xr[u][e], v[r][e]);
-                }
-        }
-    }
-    if (nres > RW) {
-        int pre = 0;
-        for (int r = 0; r < RPW && wave + WAVES * r < M; ++r) {
-            const int32_t m = d.m0 + wave + WAVES * r;
-            const int32_t rb = res_ptr[m], re = res_ptr[m + 1];
-            for (int32_t q = rb + (RW > pre ? (RW - pre < re - rb ? RW - pre : re - rb) : 0); q < re; ++q) {
-                float xr[V];
-#pragma unroll
-                for (int e = 0; e < V; ++e) xr[e] = 0.f;
-                if (act) ldv<V>(xc + (int64_t)res_col[q] * ld_x + lo, xr);
-                const float w = res_val[q];
-#pragma unroll
-                for (int rr = 0; rr < RPW; ++rr)
-                    if (rr == r) {
-#pragma unroll
-                        for (int e = 0; e < V; ++e) v[rr][e] = __builtin_fmaf(w, xr[e], v[rr][e]);
-                    }
+                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xr[q][e], v[r][e]);
             }
-            pre += re - rb;
-        }
+    }
+    // overflow: entries past the RQ held per wave, and clique entries past the RW fetched
+    // lane-parallel (scalar loads, one gather at a time)
+    for (; mine; mine &= mine - 1) {
+        const int j = __builtin_ctzll(mine);
+        const int64_t row = __builtin_amdgcn_readlane(d.rsrc, j);
+        float xo[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) xo[e] = 0.f;
+        if (act) ldv<V>(xc + row * ld_x + lo, xo);
+        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j));
+        const int slot = __builtin_amdgcn_readlane(d.rk, j) / WAVES;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+            if (slot == r) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[e], v[r][e]);
+            }
+    }
+    for (int32_t q = d.cr0 + nl; q < d.cr0 + ncr; ++q) {
+        const int k = res_member[q];
+        if (k % WAVES != wave) continue;                                // wave-uniform
+        float xo[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) xo[e] = 0.f;
+        if (act) ldv<V>(xc + (int64_t)res_col[q] * ld_x + lo, xo);
+        const float w = res_val[q];
+        const int slot = k / WAVES;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+            if (slot == r) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[e], v[r][e]);
+            }
     }
     // 4. group sums across waves through LDS (waves 0..G-1 each reduce one group)
-    __syncthreads();
-    if (wave < G) {
+    if (!NO_RED) __syncthreads();
+    if (!NO_RED && wave < G) {
         float a[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) a[e] = red[wave][0][V * lane + e];
@@ -422,12 +431,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int e = 0; e < V; ++e) tot[wave][V * lane + e] = a[e];
     }
-    __syncthreads();
+    if (!NO_RED) __syncthreads();
     float sg[G][V];
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int e = 0; e < V; ++e) sg[g][e] = tot[g][V * lane + e];
+        for (int e = 0; e < V; ++e) sg[g][e] = NO_RED ? red[g][wave][V * lane + e] : tot[g][V * lane + e];
     // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here)
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -1202,7 +1211,7 @@ void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t
     hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL, V>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
-                       pl->res_val, n_items);
+                       pl->res_val, pl->res_member, n_items);
 }
 
 template <int WAVES, int RPW, int OCC, int RW, int FL, int V>
@@ -1234,7 +1243,7 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     const int mc = pl->max_clique;
     if (!vec4) return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
     if (waves * rpw < mc) {
-        rw = 64; ob = 0; v = 4;
+        rw = 64; ob = 2; v = 4;     // non-temporal member loads: 1.39 vs 1.47 ms (headline, same box)
         if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
         else if (mc <= 32) { waves = 8; rpw = 4; occ = 8; }
         else if (mc <= 64) { waves = 16; rpw = 4; occ = 8; }
@@ -1244,10 +1253,11 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
     }
 #define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s)
-    NIIDMIX_TILE(8, 2, 8, 64, 0, 4); NIIDMIX_TILE(8, 4, 8, 64, 0, 4); NIIDMIX_TILE(16, 4, 8, 64, 0, 4);
-    NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 8, 4, 64, 0, 4); NIIDMIX_TILE(16, 16, 4, 64, 0, 4);
-    // tuning alternatives
-    NIIDMIX_TILE(16, 7, 8, 0, 0, 4); NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 0, 4);
+    NIIDMIX_TILE(8, 2, 8, 64, 2, 4); NIIDMIX_TILE(8, 4, 8, 64, 2, 4); NIIDMIX_TILE(16, 4, 8, 64, 2, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
+    // tuning alternatives / timing-only ablations
+    NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 7, 8, 0, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 2, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 6, 4); NIIDMIX_TILE(16, 7, 8, 64, 10, 4);
 #undef NIIDMIX_TILE
     return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%dx%d", waves, rpw, occ, rw, ob, v);
 }
@@ -1309,7 +1319,8 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     if (p < 0 || plan->n_cliques < 0 || plan->n_members < 0) return set_error(NIIDMIX_EINVAL, "negative size");
     if (plan->n_cliques == 0 || p == 0) return NIIDMIX_OK;
     if (!x || !y || !plan->clique_ptr || !plan->member_row || !plan->member_group || !plan->coef ||
-        !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0))
+        !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
+        (!plan->res_member && plan->n_members > 0))
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
     if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");

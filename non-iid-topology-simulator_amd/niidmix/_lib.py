@@ -26,7 +26,7 @@ class CliquePlanC(ctypes.Structure):
     """Mirror of struct niidmix_clique_plan (include/niidmix.h)."""
     _fields_ = [("n_cliques", _i32), ("n_members", _i32), ("n_groups", _i32), ("max_clique", _i32),
                 ("max_clique_res", _i32), ("clique_ptr", _vp), ("member_row", _vp), ("member_group", _vp), ("coef", _vp),
-                ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp)]
+                ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp), ("res_member", _vp)]
 
 
 class StagedPlanC(ctypes.Structure):

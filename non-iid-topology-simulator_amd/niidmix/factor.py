@@ -39,6 +39,7 @@ class CliquePlan:
     res_ptr: np.ndarray        # int32 [M+1]
     res_col: np.ndarray        # int32 [R]
     res_val: np.ndarray        # fp32 [R]
+    res_member: np.ndarray = None   # int32 [R]: the entry's member index within its clique
 
     @property
     def n_cliques(self):
@@ -134,7 +135,7 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
     M = n
     coef = np.zeros((M, 1 + G), np.float32)
     res_ptr = np.zeros(M + 1, np.int64)
-    res_cols, res_vals = [], []
+    res_cols, res_vals, res_member = [], [], []
     member_row = flat.astype(np.int32)
     member_group = group_of[flat].astype(np.int32)
     clique_ptr = np.cumsum([0] + [len(c) for c in cliques]).astype(np.int32)
@@ -177,6 +178,7 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
                     rc.append(int(j)); rv.append(-c_g)
         res_cols.extend(rc)
         res_vals.extend(rv)
+        res_member.extend([m - int(clique_ptr[ci])] * len(rc))
         res_ptr[m + 1] = res_ptr[m] + len(rc)
     n_res = int(res_ptr[-1])
     if n_res > max_res_per_node * n:
@@ -188,5 +190,6 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
                       member_row=member_row, member_group=member_group, coef=coef,
                       res_ptr=res_ptr.astype(np.int32),
                       res_col=np.asarray(res_cols, np.int32),
-                      res_val=np.asarray(res_vals, np.float64).astype(np.float32))
+                      res_val=np.asarray(res_vals, np.float64).astype(np.float32),
+                      res_member=np.asarray(res_member, np.int32))
     return plan, None

@@ -2,7 +2,7 @@
 
 Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
-  mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, out,
+  mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, res_member, out,
              max_clique, max_clique_res)            k_mix_clique_wave (fast, HBM-bound)
   mix_tile_lds(x, <tile lds plan tensors>, out, rt, max_src, max_tiles, mode)
                                                     k_mix_tile_lds (exact default, LDS-staged)
@@ -97,8 +97,8 @@ def mix_csr(x: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor, val: torc
 @torch.library.custom_op("niidmix::mix_clique", mutates_args=("out",))
 def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
                member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
-               res_col: torch.Tensor, res_val: torch.Tensor, out: torch.Tensor,
-               max_clique: int, max_clique_res: int) -> None:
+               res_col: torch.Tensor, res_val: torch.Tensor, res_member: torch.Tensor,
+               out: torch.Tensor, max_clique: int, max_clique_res: int) -> None:
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -113,13 +113,15 @@ def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tens
     _vec("res_ptr", res_ptr, torch.int32, dev, m + 1)
     _vec("res_col", res_col, torch.int32, dev)
     _vec("res_val", res_val, torch.float32, dev, res_col.numel())
+    _vec("res_member", res_member, torch.int32, dev, res_col.numel())
     _no_overlap(x, out)
     plan = _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), int(max_clique_res),
                             clique_ptr.data_ptr(),
                             member_row.data_ptr(), member_group.data_ptr(), coef.data_ptr(),
                             res_ptr.data_ptr(), res_col.data_ptr() if res_col.numel() else
                             res_ptr.data_ptr(), res_val.data_ptr() if res_val.numel() else
-                            coef.data_ptr())
+                            coef.data_ptr(), res_member.data_ptr() if res_member.numel() else
+                            res_ptr.data_ptr())
     rc = _lib.lib.niidmix_mix_clique_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
                                          ctypes.byref(plan), _stream(x))
     _lib.check(rc, "niidmix::mix_clique")
@@ -292,6 +294,7 @@ class Mixer:
             self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
             self.p_res_col = torch.from_numpy(p.res_col).to(dev)
             self.p_res_val = torch.from_numpy(p.res_val).to(dev)
+            self.p_res_member = torch.from_numpy(p.res_member).to(dev)
         self.staged, self.staged_reason = build_staged_plan(csr, cliques) if cliques else \
             build_staged_plan(csr, None)
         if self.staged is not None:
@@ -386,7 +389,8 @@ class Mixer:
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
-                       self.p_res_ptr, self.p_res_col, self.p_res_val, out, self.plan.max_clique,
+                       self.p_res_ptr, self.p_res_col, self.p_res_val, self.p_res_member, out,
+                       self.plan.max_clique,
                        self.plan.max_clique_res)
         elif k == "dense":
             w = self.w_dense if self.w_dense is not None else \

@@ -49,10 +49,10 @@ def test_argument_errors_without_gpu():
     rc = L.niidmix_mix_csr_f32(16, 2, 1024, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EINVAL        # ld < p
     assert L.niidmix_mix_csr_f32(16, 4, 1024, 4, 0, 4, 8, 8, 8, 0, None) == _lib.OK  # empty
-    plan = _lib.CliquePlanC(1, 4, 5, 4, 0, 8, 8, 8, 8, 8, 8, 8)
+    plan = _lib.CliquePlanC(1, 4, 5, 4, 0, 8, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
     assert rc == _lib.EUNSUPPORTED   # n_groups 5
-    plan = _lib.CliquePlanC(1, 300, 2, 300, -1, 8, 8, 8, 8, 8, 8, 8)
+    plan = _lib.CliquePlanC(1, 300, 2, 300, -1, 8, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
     assert rc == _lib.EINVAL         # negative max_clique_res
     sp = _lib.StagedPlanC(1, 300, 8, 8, 8, 8, 8, 8, 8)
