@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident round (pinned [N,P] host slab -> H2D -> mix -> "
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
+    ap.add_argument("--hipmalloc-slabs", action="store_true",
+                    help="single GPU: allocate the slabs with torch's default (hipMalloc) allocator "
+                         "instead of the VMM-mapped slab pool")
     ap.add_argument("--ld-pad", type=int, default=0,
                     help="single GPU: pad every slab row by this many floats (ld = P + pad)")
     ap.add_argument("--workload", default="mix", choices=["mix", "grad-clique"],
@@ -277,7 +280,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from niidmix import ops
+    from niidmix import memory, ops
     if args.workload != "mix" and world > 1:
         raise SystemExit("--workload grad-clique is single-GPU")
     if world == 1:
@@ -298,8 +301,14 @@ def main():
         parallelism = "single GPU"
         gen = torch.Generator(device=dev).manual_seed(args.seed)
         ld = p + args.ld_pad
-        xa = torch.randn(n_local, ld, device=dev, generator=gen)[:, :p]
-        xb = torch.empty(n_local, ld, device=dev)[:, :p]
+        # node-state slabs in VMM-mapped HBM (niidmix.memory); --hipmalloc-slabs:
+        # torch's default allocator instead (placement-dependent speed, for comparison)
+        alloc = (lambda: torch.empty(n_local, ld, device=dev)) if args.hipmalloc_slabs else \
+            (lambda: memory.empty_slab(n_local, ld, dev))
+        xa = alloc()
+        xa.normal_(generator=gen)
+        xa = xa[:, :p]
+        xb = alloc()[:, :p]
         halo = 0
     else:
         from niidmix.shard import ShardedMixer
@@ -410,6 +419,8 @@ def main():
                        "mode": mode, "parallelism": parallelism,
                        "launch_ms": round(launch_ms, 4), "halo_rows_rank0": halo,
                        "hipgraph": graph is not None,
+                       "slab_memory": ("hipMalloc" if args.hipmalloc_slabs or world > 1
+                                       else "VMM 2 MiB chunks (niidmix_hbm_alloc)"),
                        "stream_copy_GBs": round(copy_gbs, 1),
                        "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
                                                if roof["unit"] == "GB/s" else None)},

@@ -25,6 +25,7 @@
 #define NIIDMIX_H
 
 #include <stdint.h>
+#include <sys/types.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -249,6 +250,16 @@ int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
 int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t p,
                                   int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
                                   void *stream);
+
+/* Device memory for node-state slabs, with the signatures of a PyTorch pluggable allocator
+ * (torch.cuda.memory.CUDAPluggableAllocator; niidmix.memory.slab_pool uses them for a MemPool).
+ * The range is reserved with hipMemAddressReserve and mapped from 2 MiB physical chunks
+ * (hipMemCreate / hipMemMap): the clique kernel's access pattern measured 1.32 ms per headline round
+ * on every such slab, against 1.35-1.64 ms on hipMalloc'ed slabs depending on their physical
+ * placement.  Returns NULL on failure (niidmix_last_error says why); free with
+ * niidmix_hbm_free (size, device and stream are ignored). */
+void *niidmix_hbm_alloc(ssize_t size, int device, void *stream);
+void niidmix_hbm_free(void *ptr, ssize_t size, int device, void *stream);
 
 /* Strided host <-> device copy (hipMemcpy2DAsync) of `rows` rows of `width_bytes` each, used by
  * the host-resident drop-in (niidmix.slab) to stream column windows of the pinned [N, P] host slab

@@ -31,6 +31,11 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/types.h>
+
+#include <mutex>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/niidmix.h"
 
@@ -212,6 +217,18 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
 //   3. y_m = a_m x_m + sum_g c_{m,g} S_g + residual terms (gateway edges), stored once (nt).
 // Work order is XCD-aware (the cliques of one chunk run back to back on one XCD) so the residual
 // rows a gateway gathers from another clique are normally still in that XCD's L2.
+// Work item t -> (chunk, clique).  XCD-aware: items t and t+8 share an XCD and consecutive items
+// of one XCD sweep the cliques of one chunk.  skew (a multiple of 8 chunks, or 0) rotates each
+// clique's chunk sequence by cq*skew, so the cliques in flight together read different column
+// offsets (tuning: spreads the rows' concurrent addresses over more HBM channels).
+__device__ __forceinline__ void clique_item(int64_t t, int32_t n_cliques, int64_t nc, int64_t skew,
+                                            int64_t &chunk, int32_t &cq) {
+    const int64_t local = t >> 3;
+    const int64_t base = (local / n_cliques) * 8 + (t & 7);
+    cq = (int32_t)(local % n_cliques);
+    chunk = (skew && base < nc) ? (base + (int64_t)cq * skew) % nc : base;
+}
+
 template <int G, int RW>
 struct CliqueDesc {        // one work item's descriptors, lane-parallel
     int32_t m0, M;         // wave-uniform: first member, members (0 past p)
@@ -235,10 +252,11 @@ __device__ __forceinline__ void load_clique_desc(CliqueDesc<G, RW> &d, int64_t t
                                                  const int32_t *__restrict__ res_ptr,
                                                  const int32_t *__restrict__ res_col,
                                                  const float *__restrict__ res_val,
-                                                 const int32_t *__restrict__ res_member) {
-    const int64_t local = t >> 3;
-    const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
-    const int32_t cq = (int32_t)(local % n_cliques);
+                                                 const int32_t *__restrict__ res_member,
+                                                 int64_t skew) {
+    int64_t chunk;
+    int32_t cq;
+    clique_item(t, n_cliques, (p + CW - 1) / CW, skew, chunk, cq);
     const bool valid = chunk * CW < p;
     d.m0 = clique_ptr[cq];
     const int32_t m1 = clique_ptr[cq + 1];
@@ -279,13 +297,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val,
-    const int32_t *__restrict__ res_member, int64_t n_items) {
+    const int32_t *__restrict__ res_member, int64_t n_items, int64_t skew) {
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
     static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
     // timing-only ablations (WRONG results; tools/tune_inproc.py): 4 = skip residual gathers,
     // 8 = skip the cross-wave LDS reduction (per-wave group sums only, no barriers)
     constexpr bool NO_RES = (FL & 4) != 0, NO_RED = (FL & 8) != 0;
+    constexpr bool PLAIN_ST = (FL & 16) != 0;   // write-back (L2) stores instead of non-temporal
     constexpr int RQ = 2;                     // residual rows per wave held in registers
     constexpr int64_t CW = 64 * V;            // columns per work item
     __shared__ float red[G][WAVES][kWave * V];
@@ -297,9 +316,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     CliqueDesc<G, RW> d;
     load_clique_desc<WAVES, RPW, G, RW, CW>(d, t, n_cliques, p, wave, lane, clique_ptr, member_row,
                                             member_group, coef, res_ptr, res_col, res_val,
-                                            res_member);
-    const int64_t local = t >> 3;
-    const int64_t chunk = (local / n_cliques) * 8 + (t & 7);
+                                            res_member, skew);
+    int64_t chunk;
+    int32_t cq_unused;
+    clique_item(t, n_cliques, (p + CW - 1) / CW, skew, chunk, cq_unused);
     const bool act = chunk * CW + V * lane < p;
     const int32_t M = d.M;
     const float *xc = x + chunk * CW;
@@ -448,7 +468,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(cg, sg[g][e], v[r][e]);
             }
             const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-            if (act) stv_nt<V>(yc + row * ld_y + lo, v[r]);
+            if (act) {
+                if (PLAIN_ST) *reinterpret_cast<float4 *>(yc + row * ld_y + lo) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+                else stv_nt<V>(yc + row * ld_y + lo, v[r]);
+            }
         }
     }
 }
@@ -1204,6 +1227,13 @@ bool overlaps(const float *a, int64_t a_elems, const float *b, int64_t b_elems) 
     return a < b + b_elems && b < a + a_elems;
 }
 
+// NIIDMIX_CLIQUE_SKEW=<chunks> (multiple of 8; tuning): per-clique chunk rotation, 0 = off
+int64_t clique_skew() {
+    const char *e = getenv("NIIDMIX_CLIQUE_SKEW");
+    const int64_t v = e ? atoll(e) : 0;
+    return v > 0 ? (v + 7) / 8 * 8 : 0;
+}
+
 template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                    const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
@@ -1211,7 +1241,7 @@ void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t
     hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL, V>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
-                       pl->res_val, pl->res_member, n_items);
+                       pl->res_val, pl->res_member, n_items, clique_skew());
 }
 
 template <int WAVES, int RPW, int OCC, int RW, int FL, int V>
@@ -1257,14 +1287,116 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
     // tuning alternatives / timing-only ablations
     NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 7, 8, 0, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 2, 4);
-    NIIDMIX_TILE(16, 7, 8, 64, 6, 4); NIIDMIX_TILE(16, 7, 8, 64, 10, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 6, 4); NIIDMIX_TILE(16, 7, 8, 64, 10, 4); NIIDMIX_TILE(16, 7, 8, 64, 18, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 16, 4);
 #undef NIIDMIX_TILE
     return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%dx%d", waves, rpw, occ, rw, ob, v);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Node-state slab memory.  Measured (tools/hbm_probe7.hip): the clique access pattern (100 rows of
+// a clique x 1 KiB column chunk, all cliques of a chunk in flight together) runs at 1.32 ms on
+// slabs mapped from 2 MiB physical chunks through the HIP virtual-memory API on every allocation
+// tried, but at 1.35-1.64 ms on hipMalloc'ed slabs depending on where the driver places them (a
+// physically contiguous hipExtMallocWithFlags slab: 1.49-1.57 ms every time; a linear copy is
+// unaffected).  niidmix_hbm_alloc therefore reserves a VA range and maps it chunk by chunk.
+struct HbmBlock {
+    size_t bytes;
+    std::vector<hipMemGenericAllocationHandle_t> chunks;
+    std::vector<size_t> slot;        // VA chunk slot of chunks[i]
+};
+// never destroyed: frees may arrive from other libraries' teardown after static destruction began
+std::mutex &g_hbm_mu = *new std::mutex;
+std::unordered_map<void *, HbmBlock> &g_hbm = *new std::unordered_map<void *, HbmBlock>;
+constexpr size_t kHbmChunk = 2u << 20;
+
+void hbm_release(void *va, HbmBlock &b, size_t mapped) {
+    for (size_t i = 0; i < mapped; ++i) (void)hipMemUnmap((char *)va + b.slot[i] * kHbmChunk, kHbmChunk);
+    for (auto h : b.chunks) (void)hipMemRelease(h);
+    (void)hipMemAddressFree(va, b.bytes);
 }
 
 }  // namespace
 
 extern "C" {
+
+void *niidmix_hbm_alloc(ssize_t size, int device, void *stream) {
+    (void)stream;
+    if (size <= 0) return nullptr;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess ||
+        gran == 0 || kHbmChunk % gran != 0) {
+        set_error(NIIDMIX_EHIP, "hbm_alloc: no usable VMM granularity");
+        return nullptr;
+    }
+    HbmBlock b;
+    const size_t n = ((size_t)size + kHbmChunk - 1) / kHbmChunk;
+    b.bytes = n * kHbmChunk;
+    void *va = nullptr;
+    if (hipMemAddressReserve(&va, b.bytes, kHbmChunk, nullptr, 0) != hipSuccess) {
+        set_error(NIIDMIX_EHIP, "hbm_alloc: VA reservation of %zu B failed", b.bytes);
+        return nullptr;
+    }
+    b.chunks.reserve(n);
+    bool ok = true;
+    for (size_t i = 0; i < n && ok; ++i) {
+        hipMemGenericAllocationHandle_t h;
+        if (hipMemCreate(&h, kHbmChunk, &prop, 0) != hipSuccess) { ok = false; break; }
+        b.chunks.push_back(h);
+    }
+    // chunk i goes to VA slot slot[i], a fixed pseudo-random permutation (Fisher-Yates over
+    // xorshift64), so consecutive VA chunks do not sit on consecutive physical chunks even when
+    // the driver hands them out in order
+    std::vector<size_t> slot(b.chunks.size());
+    for (size_t i = 0; i < slot.size(); ++i) slot[i] = i;
+    uint64_t st = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    for (size_t i = slot.size(); i > 1; --i) {
+        st ^= st << 13; st ^= st >> 7; st ^= st << 17;                 // xorshift64
+        const size_t j = (size_t)(st % i);
+        const size_t t = slot[i - 1]; slot[i - 1] = slot[j]; slot[j] = t;
+    }
+    b.slot = slot;
+    size_t mapped = 0;
+    for (size_t i = 0; i < b.chunks.size() && ok; ++i) {
+        if (hipMemMap((char *)va + b.slot[i] * kHbmChunk, kHbmChunk, 0, b.chunks[i], 0) != hipSuccess) { ok = false; break; }
+        ++mapped;
+    }
+    if (ok) {
+        hipMemAccessDesc d = {};
+        d.location.type = hipMemLocationTypeDevice;
+        d.location.id = device;
+        d.flags = hipMemAccessFlagsProtReadWrite;
+        ok = hipMemSetAccess(va, b.bytes, &d, 1) == hipSuccess;
+    }
+    if (!ok) {
+        hbm_release(va, b, mapped);
+        set_error(NIIDMIX_EHIP, "hbm_alloc: mapping %zu B failed (out of device memory?)", b.bytes);
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    g_hbm.emplace(va, std::move(b));
+    return va;
+}
+
+void niidmix_hbm_free(void *ptr, ssize_t size, int device, void *stream) {
+    (void)size; (void)device; (void)stream;
+    if (!ptr) return;
+    HbmBlock b;
+    {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        auto it = g_hbm.find(ptr);
+        if (it == g_hbm.end()) return;
+        b = std::move(it->second);
+        g_hbm.erase(it);
+    }
+    (void)hipDeviceSynchronize();          // the caching allocator frees only idle blocks; be safe
+    hbm_release(ptr, b, b.chunks.size());
+}
+
 
 int niidmix_abi_version(void) { return NIIDMIX_ABI_VERSION; }
 

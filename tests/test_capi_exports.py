@@ -9,13 +9,16 @@ from conftest import REPO
 
 def _declared_symbols():
     text = open(os.path.join(REPO, "include", "niidmix.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(niidmix_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void \*|void)\s*(niidmix_\w+)\s*\(",
+                                 text, re.M)))
 
 
 def test_header_declares_expected_api():
     syms = _declared_symbols()
     for s in ["niidmix_abi_version", "niidmix_last_error", "niidmix_mix_csr_f32",
-              "niidmix_mix_clique_f32", "niidmix_mix_dense_f32", "niidmix_mean_rows_f32"]:
+              "niidmix_mix_clique_f32", "niidmix_mix_dense_f32", "niidmix_mean_rows_f32",
+              "niidmix_mix_tile_lds_f32", "niidmix_grad_segment_mean_f32", "niidmix_hbm_alloc",
+              "niidmix_hbm_free"]:
         assert s in syms
 
 

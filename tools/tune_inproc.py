@@ -33,8 +33,14 @@ def main():
     csr, cl, p0, desc = bench.single_gpu_topology(a.config)
     p = a.p or p0
     m = ops.Mixer(csr=csr, cliques=cl, device=dev)
-    x = torch.randn(csr.n, p, device=dev)
-    y = torch.empty_like(x)
+    from niidmix import memory
+    if os.environ.get("TUNE_HIPMALLOC"):
+        x = torch.randn(csr.n, p, device=dev)
+        y = torch.empty_like(x)
+    else:
+        x = memory.empty_slab(csr.n, p, dev)
+        x.normal_()
+        y = memory.empty_slab(csr.n, p, dev)
     variants = []
     for v in a.variant or ["wave::clique"]:
         name, env, kernel = v.split(":")
