@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident round (pinned [N,P] host slab -> H2D -> mix -> "
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
+    ap.add_argument("--layout", default="blocked", choices=["blocked", "rowmajor"],
+                    help="single GPU, clique kernel: device-resident slabs column-blocked "
+                         "[P/4096, N, 4096] (default) or row-major [N, P]")
     ap.add_argument("--hipmalloc-slabs", action="store_true",
                     help="single GPU: allocate the slabs with torch's default (hipMalloc) allocator "
                          "instead of the VMM-mapped slab pool")
@@ -310,6 +313,12 @@ def main():
         xa = xa[:, :p]
         xb = alloc()[:, :p]
         halo = 0
+        k0 = args.kernel if args.kernel != "auto" else mixer.kernel_for("fast", xa)
+        if args.layout == "blocked" and k0 == "clique" and args.workload == "mix":
+            # device-resident node state in the column-blocked layout [K, N, 4096]
+            xa = memory.to_blocked(xa)
+            xb = memory.empty_blocked(n_local, p, dev)
+            torch.cuda.empty_cache()
     else:
         from niidmix.shard import ShardedMixer
         p = args.p or (1 << 20)
@@ -330,11 +339,18 @@ def main():
     kernel = args.kernel if args.kernel != "auto" else mixer.kernel_for("fast", xa)
     mode = "exact" if kernel.endswith("exact") else "fast"
 
+    blocked = world == 1 and xa.dim() == 3
+    if blocked:
+        kernel = "clique"
+
     def step(a, b, evs=None):
         if world == 1:
             if evs is not None:
                 evs[0].record(torch.cuda.current_stream(dev))
-            mixer(a, out=b, kernel=kernel, mode=mode)
+            if blocked:
+                mixer.mix_blocked(a, b, p)
+            else:
+                mixer(a, out=b, kernel=kernel, mode=mode)
             if evs is not None:
                 evs[1].record(torch.cuda.current_stream(dev))
         else:
@@ -421,6 +437,8 @@ def main():
                        "hipgraph": graph is not None,
                        "slab_memory": ("hipMalloc" if args.hipmalloc_slabs or world > 1
                                        else "VMM 2 MiB chunks (niidmix_hbm_alloc)"),
+                       "slab_layout": (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, "
+                                       f"{xa.shape[2]}]" if blocked else "row-major [N, P]"),
                        "stream_copy_GBs": round(copy_gbs, 1),
                        "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
                                                if roof["unit"] == "GB/s" else None)},

@@ -157,6 +157,18 @@ typedef struct niidmix_staged_plan {
 int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                            const niidmix_staged_plan *plan, int mode, void *stream);
 
+/* The same clique-factored round on COLUMN-BLOCKED slabs: x and y are [K][rows][block_cols]
+ * (K = ceil(p / block_cols) blocks of row-major [rows, block_cols] sub-slabs with row stride `ld`
+ * floats and block strides block_stride_x / block_stride_y floats), element (r, c) at
+ *   base + (c / block_cols) * block_stride + r * ld + c % block_cols.
+ * block_cols: a power of two >= 256.  This is the layout niidmix keeps device-resident node state
+ * in (block_cols = 4096): a clique's member rows then sit 16 KiB apart instead of P*4 bytes, which
+ * measured robust to the slab's physical placement.  Cliques of <= 256 members. */
+int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
+                                   int64_t block_cols, int64_t block_stride_x,
+                                   int64_t block_stride_y, const niidmix_clique_plan *plan,
+                                   void *stream);
+
 /* Merged-order row tiles, exact or fast: the same result as niidmix_mix_csr_f32 (bit for bit in
  * NIIDMIX_MODE_EXACT: every row keeps its own operand order — self, then edges[rank] in list order,
  * d_sgd.py:105-106 — and its own roundings), computed so that rows sharing sources share the loads.

@@ -297,7 +297,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val,
-    const int32_t *__restrict__ res_member, int64_t n_items, int64_t skew) {
+    const int32_t *__restrict__ res_member, int64_t n_items, int64_t skew, int cpb_shift,
+    int64_t bs_x, int64_t bs_y) {
+    // column-blocked slabs ([K][rows][B], B = CW << cpb_shift columns, block strides bs_x / bs_y
+    // floats; a row-major slab is one block: cpb_shift = 62): chunk c lives in block c >> cpb_shift
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
     static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
@@ -322,8 +325,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     clique_item(t, n_cliques, (p + CW - 1) / CW, skew, chunk, cq_unused);
     const bool act = chunk * CW + V * lane < p;
     const int32_t M = d.M;
-    const float *xc = x + chunk * CW;
-    float *yc = y + chunk * CW;
+    const int64_t kb = chunk >> cpb_shift, cin = chunk - (kb << cpb_shift);
+    const float *xc = x + kb * bs_x + cin * CW;
+    float *yc = y + kb * bs_y + cin * CW;
     const unsigned lo = (unsigned)(V * lane);
 
     // 1. member rows -> registers, all loads in flight before the first use
@@ -1234,27 +1238,33 @@ int64_t clique_skew() {
     return v > 0 ? (v + 7) / 8 * 8 : 0;
 }
 
+struct BlockGeom {            // column blocking of the slabs (row-major: one block)
+    int cpb_shift = 62;        // 256-column chunks per block = 1 << cpb_shift
+    int64_t bs_x = 0, bs_y = 0;
+};
+
 template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
 void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                   const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s) {
+                   const niidmix_clique_plan *pl, int64_t n_items, hipStream_t s, const BlockGeom &bg) {
     const int64_t grid = n_items;   // one block per (clique, chunk) item; < 2^31 checked by the caller
     hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL, V>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
-                       pl->res_val, pl->res_member, n_items, clique_skew());
+                       pl->res_val, pl->res_member, n_items, clique_skew(), bg.cpb_shift, bg.bs_x,
+                       bg.bs_y);
 }
 
 template <int WAVES, int RPW, int OCC, int RW, int FL, int V>
 int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                    const niidmix_clique_plan *pl, hipStream_t s) {
+                    const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
     const int64_t n_chunks = (p + 64 * V - 1) / (64 * V);
     const int64_t n_items = (int64_t)pl->n_cliques * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique, chunk) items for one grid");
     switch (pl->n_groups) {
-        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
-        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s); break;
+        case 1: launch_clique<WAVES, RPW, 1, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s, bg); break;
+        case 2: launch_clique<WAVES, RPW, 2, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s, bg); break;
+        case 3: launch_clique<WAVES, RPW, 3, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s, bg); break;
+        case 4: launch_clique<WAVES, RPW, 4, OCC, RW, FL, V>(x, ld_x, y, ld_y, p, pl, n_items, s, bg); break;
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
     return check_launch("k_mix_clique");
@@ -1266,7 +1276,8 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 // slab allows float4 access and the clique fits 256 rows, else 1).
 // NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>x<v> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                        const niidmix_clique_plan *pl, bool vec4, hipStream_t s) {
+                        const niidmix_clique_plan *pl, bool vec4, hipStream_t s,
+                        const BlockGeom &bg = BlockGeom()) {
     int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0, v = 0;
     if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob, &v);
     if (v == 0) v = 4;
@@ -1282,7 +1293,7 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         else if (mc <= 256) { waves = 16; rpw = 16; occ = 4; }
         else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
     }
-#define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s)
+#define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s, bg)
     NIIDMIX_TILE(8, 2, 8, 64, 2, 4); NIIDMIX_TILE(8, 4, 8, 64, 2, 4); NIIDMIX_TILE(16, 4, 8, 64, 2, 4);
     NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
     // tuning alternatives / timing-only ablations
@@ -1443,6 +1454,34 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 #undef NIIDMIX_CSR_S
 #undef NIIDMIX_CSR
     return check_launch("k_mix_csr");
+}
+
+int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
+                                   int64_t block_cols, int64_t block_stride_x,
+                                   int64_t block_stride_y, const niidmix_clique_plan *plan,
+                                   void *stream) {
+    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
+    if (p < 0 || plan->n_cliques < 0 || plan->n_members < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (plan->n_cliques == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !plan->clique_ptr || !plan->member_row || !plan->member_group || !plan->coef ||
+        !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
+        (!plan->res_member && plan->n_members > 0))
+        return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (block_cols < 256 || (block_cols & (block_cols - 1)))
+        return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= 256", (long long)block_cols);
+    if (ld < block_cols) return set_error(NIIDMIX_EINVAL, "row stride < block_cols");
+    if (block_stride_x < ld || block_stride_y < ld)
+        return set_error(NIIDMIX_EINVAL, "block stride < row stride");
+    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (plan->max_clique > 256) return set_error(NIIDMIX_EUNSUPPORTED, "blocked slabs: cliques of <= 256 members");
+    if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
+    const bool vec4 = (ld % 4 == 0) && (block_stride_x % 4 == 0) && (block_stride_y % 4 == 0) &&
+                      aligned16(x) && aligned16(y);
+    BlockGeom bg;
+    bg.cpb_shift = __builtin_ctzll((unsigned long long)(block_cols / 256));
+    bg.bs_x = block_stride_x;
+    bg.bs_y = block_stride_y;
+    return launch_clique_tiled(x, ld, y, ld, p, plan, vec4, reinterpret_cast<hipStream_t>(stream), bg);
 }
 
 int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,

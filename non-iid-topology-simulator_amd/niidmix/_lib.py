@@ -57,6 +57,8 @@ SIGNATURES = {
                                            ctypes.c_int, _vp]),
     "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(CliquePlanC), _vp]),
+    "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                                      ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_staged_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(StagedPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,

@@ -47,3 +47,43 @@ def empty_slab(rows, cols, device, dtype=torch.float32):
     """An uninitialised [rows, cols] tensor in VMM-backed slab memory on `device`."""
     with slabs(device):
         return torch.empty((rows, cols), dtype=dtype, device=device)
+
+
+BLOCK_COLS = 4096
+
+
+def empty_blocked(rows, p, device, block_cols=BLOCK_COLS):
+    """An uninitialised COLUMN-BLOCKED slab [K, rows, block_cols] (K = ceil(p / block_cols)) in
+    VMM-backed slab memory: the device-resident layout of node state for the clique kernel.
+    Element (r, c) of the logical [rows, p] slab is x[c // block_cols, r, c % block_cols].  A
+    clique's member rows are block_cols*4 bytes apart instead of p*4, which measured robust to the
+    slab's physical placement (tools/hbm_probe7.hip)."""
+    k = (p + block_cols - 1) // block_cols
+    with slabs(device):
+        return torch.empty((k, rows, block_cols), dtype=torch.float32, device=device)
+
+
+def to_blocked(x, block_cols=BLOCK_COLS, out=None):
+    """Row-major [rows, p] -> column-blocked [K, rows, block_cols] (padding columns zeroed)."""
+    rows, p = x.shape
+    if out is None:
+        out = empty_blocked(rows, p, x.device, block_cols) if x.is_cuda else \
+            torch.empty(((p + block_cols - 1) // block_cols, rows, block_cols), dtype=x.dtype)
+    k = out.shape[0]
+    for i in range(k):
+        c0, c1 = i * block_cols, min(p, (i + 1) * block_cols)
+        out[i, :, :c1 - c0].copy_(x[:, c0:c1])
+        if c1 - c0 < block_cols:
+            out[i, :, c1 - c0:].zero_()
+    return out
+
+
+def from_blocked(xb, p, out=None):
+    """Column-blocked [K, rows, B] -> row-major [rows, p]."""
+    k, rows, b = xb.shape
+    if out is None:
+        out = torch.empty((rows, p), dtype=xb.dtype, device=xb.device)
+    for i in range(k):
+        c0, c1 = i * b, min(p, (i + 1) * b)
+        out[:, c0:c1].copy_(xb[i, :, :c1 - c0])
+    return out

@@ -101,7 +101,18 @@ def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tens
                out: torch.Tensor, max_clique: int, max_clique_res: int) -> None:
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
-    dev = x.device
+    _req(member_row.device == x.device, "plan and slabs must be on the same device")
+    _no_overlap(x, out)
+    plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
+                          res_member, max_clique, max_clique_res)
+    rc = _lib.lib.niidmix_mix_clique_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
+                                         ctypes.byref(plan), _stream(x))
+    _lib.check(rc, "niidmix::mix_clique")
+
+
+def _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
+                   res_member, max_clique, max_clique_res):
+    dev = member_row.device
     _vec("clique_ptr", clique_ptr, torch.int32, dev)
     m = member_row.numel()
     _vec("member_row", member_row, torch.int32, dev)
@@ -114,17 +125,36 @@ def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tens
     _vec("res_col", res_col, torch.int32, dev)
     _vec("res_val", res_val, torch.float32, dev, res_col.numel())
     _vec("res_member", res_member, torch.int32, dev, res_col.numel())
-    _no_overlap(x, out)
-    plan = _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), int(max_clique_res),
+    return _lib.CliquePlanC(clique_ptr.numel() - 1, m, g, int(max_clique), int(max_clique_res),
                             clique_ptr.data_ptr(),
                             member_row.data_ptr(), member_group.data_ptr(), coef.data_ptr(),
                             res_ptr.data_ptr(), res_col.data_ptr() if res_col.numel() else
                             res_ptr.data_ptr(), res_val.data_ptr() if res_val.numel() else
                             coef.data_ptr(), res_member.data_ptr() if res_member.numel() else
                             res_ptr.data_ptr())
-    rc = _lib.lib.niidmix_mix_clique_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
-                                         ctypes.byref(plan), _stream(x))
-    _lib.check(rc, "niidmix::mix_clique")
+
+
+@torch.library.custom_op("niidmix::mix_clique_blocked", mutates_args=("out",))
+def mix_clique_blocked(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
+                       member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
+                       res_col: torch.Tensor, res_val: torch.Tensor, res_member: torch.Tensor,
+                       out: torch.Tensor, p: int, max_clique: int, max_clique_res: int) -> None:
+    """Clique-factored round on column-blocked slabs x, out: [K, rows, B] (niidmix.memory)."""
+    for name, t in (("x", x), ("out", out)):
+        _req(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and
+             t.dim() == 3 and t.stride(2) == 1,
+             f"{name}: expected a HIP fp32 [K, rows, B] blocked slab with unit column stride")
+    _req(x.shape == out.shape and x.stride(1) == out.stride(1), "x and out: same blocked geometry")
+    k, rows, b = x.shape
+    _req(0 <= p <= k * b and (k == 0 or p > (k - 1) * b), f"p={p} does not fit {k} blocks of {b}")
+    _req(member_row.device == x.device, "plan and slabs must be on the same device")
+    _req(x.data_ptr() != out.data_ptr(), "x and out overlap: mixing is out-of-place")
+    plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
+                          res_member, max_clique, max_clique_res)
+    rc = _lib.lib.niidmix_mix_clique_blocked_f32(x.data_ptr(), out.data_ptr(), int(p), x.stride(1),
+                                                 b, x.stride(0), out.stride(0),
+                                                 ctypes.byref(plan), _stream(x))
+    _lib.check(rc, "niidmix::mix_clique_blocked")
 
 
 @torch.library.custom_op("niidmix::mix_staged", mutates_args=("out",))
@@ -345,6 +375,18 @@ class Mixer:
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
         self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
+
+    def mix_blocked(self, x, out, p, mode="fast", kernel=None):
+        """One round on column-blocked slabs [K, rows, B] (niidmix.memory.empty_blocked): the
+        clique-factored kernel (the device-resident fast path)."""
+        _req(mode == "fast" and kernel in (None, "clique"),
+             "blocked slabs: only the clique kernel (fast mode) reads the blocked layout")
+        _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
+        mix_clique_blocked(x, self.p_clique_ptr, self.p_member_row, self.p_member_group,
+                           self.p_coef, self.p_res_ptr, self.p_res_col, self.p_res_val,
+                           self.p_res_member, out, int(p), self.plan.max_clique,
+                           self.plan.max_clique_res)
+        return out
 
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":

@@ -41,3 +41,28 @@ def test_kernels_on_slab_memory_bitwise(gpu, oracle_mod):
     bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
     ok, worst = oracle_mod.check_tolerance(y.cpu().numpy(), g["y"], bound, rtol=1e-5)
     assert ok, worst
+
+
+@pytest.mark.parametrize("p", [64, 4096, 10_000, 3 * 4096 + 256])
+def test_blocked_clique_equals_rowmajor(p, gpu, oracle_mod):
+    """The clique kernel on column-blocked slabs [K, N, 4096] gives bit-identical results to the
+    row-major kernel (same arithmetic, different addresses), partial last block included."""
+    from niidmix import memory, ops
+    g = load_golden("dcliques1000_fc_p64")
+    m = ops.Mixer(csr=ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"]), cliques=g["cliques"],
+                  device=gpu)
+    gen = torch.Generator(device=gpu).manual_seed(p)
+    x = torch.randn(1000, p, device=gpu, generator=gen)
+    y_ref = m(x, kernel="clique")
+    xb = memory.to_blocked(x)
+    yb = memory.empty_blocked(1000, p, gpu)
+    m.mix_blocked(xb, yb, p)
+    y = memory.from_blocked(yb, p)
+    assert torch.equal(y, y_ref)
+    if p == 64:
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        xg = memory.to_blocked(torch.from_numpy(g["x"]).to(gpu))
+        m.mix_blocked(xg, yb, 64)
+        ok, worst = oracle_mod.check_tolerance(memory.from_blocked(yb, 64).cpu().numpy(), g["y"],
+                                               bound, rtol=1e-5)
+        assert ok, worst

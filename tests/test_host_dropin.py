@@ -50,3 +50,15 @@ def test_cli_registers_plugin(tmp_path):
     alg = meta.params(d, "algorithm")
     assert alg["module"] == "niidmix.d_sgd" and alg["batch-size"] == 125
     assert alg["mixing-mode"] == "exact"
+
+
+def test_blocked_layout_roundtrip_cpu():
+    """niidmix.memory.to_blocked / from_blocked: [rows, p] <-> [ceil(p/B), rows, B]."""
+    import torch
+    from niidmix import memory
+    x = torch.arange(5 * 9000, dtype=torch.float32).view(5, 9000)
+    xb = memory.to_blocked(x, block_cols=4096)
+    assert xb.shape == (3, 5, 4096)
+    assert torch.equal(xb[1, 2, :10], x[2, 4096:4106])
+    assert float(xb[2, :, 9000 - 8192:].abs().sum()) == 0.0
+    assert torch.equal(memory.from_blocked(xb, 9000), x)
