@@ -144,11 +144,11 @@ def stream_copy_probe(numel, dev, iters=10):
 
 def e2e_rounds(mixer, n, p, dev, rounds=3):
     """Host-resident round as the drop-in runs it (niidmix.slab.SlabMixer): pinned host slab,
-    H2D / mix / D2H pipelined over 64K-column windows on three streams."""
+    H2D / mix / D2H pipelined over 32K-column windows on three streams."""
     from niidmix.slab import SlabMixer
     host = torch.empty((n, p), dtype=torch.float32, pin_memory=True)
     host.normal_()
-    runner = SlabMixer(mixer, n, p, dev, window=1 << 16)
+    runner = SlabMixer(mixer, n, p, dev, window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
     res = {}
     for mode in ("fast", "exact"):
         runner.mix(host, mode=mode)                     # warm-up
@@ -314,7 +314,8 @@ def main():
         xb = alloc()[:, :p]
         halo = 0
         k0 = args.kernel if args.kernel != "auto" else mixer.kernel_for("fast", xa)
-        if args.layout == "blocked" and k0 == "clique" and args.workload == "mix":
+        if (args.layout == "blocked" and k0 == "clique" and args.workload == "mix"
+                and mixer.plan.max_clique <= 256):
             # device-resident node state in the column-blocked layout [K, N, 4096]
             xa = memory.to_blocked(xa)
             xb = memory.empty_blocked(n_local, p, dev)

@@ -91,7 +91,7 @@ class _GradEngine:
         self.slab = NodeSlab([n["model"] for n in nodes], grads=True)
         self.op = GradMean(self.plan, device)
         self.runner = SlabMixer(self.op, self.slab.n, self.slab.p, device,
-                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 16)))
+                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
 
     def valid_for(self, nodes, topology, params):
         return (topology is self.topology and _grad_key(params) == self.key
@@ -149,7 +149,7 @@ class _Engine:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=device)
         self.runner = SlabMixer(self.mixer, self.slab.n, self.slab.p, device,
-                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 16)))
+                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
 
     def valid_for(self, nodes, topology):
         return (topology is self.topology and id(topology.get("weights")) == self.weights_id

@@ -95,7 +95,7 @@ def _copy2d(dst, dpitch, src, spitch, width, rows, kind, stream):
 class SlabMixer:
     """One mixing round of a host [N, P] slab through the GPU, pipelined over column windows."""
 
-    def __init__(self, mixer, n, p, device, window=1 << 16):
+    def __init__(self, mixer, n, p, device, window=1 << 15):
         self.mixer = mixer
         self.n, self.p = n, p
         self.device = torch.device(device)
