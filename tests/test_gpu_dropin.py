@@ -158,6 +158,63 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
         assert torch.equal(u, v)
 
 
+def test_training_rounds_clique_gradient(gpu, oracle_mod):
+    """Rounds with --clique-gradient (2 cliques of 2, linear model): the drop-in's GPU gradient
+    averaging through the pinned gradient slab (kept across rounds by in-place zero_grad) gives
+    the same parameters, bit for bit, as the reference's CPU clique-gradient loop."""
+    from niidmix import d_sgd
+
+    def run(grad):
+        torch.manual_seed(1337)
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
+                  "topology": {"name": "d-cliques", "remove-clique-edges": 0},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 50,
+                                "initial-averaging": False, "clique-gradient": True,
+                                "unbiased-gradient": False}}
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc = torch.nn.Linear(784, 10)
+
+            def forward(self, x, params):
+                return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+        g = torch.Generator().manual_seed(11)
+        data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+                for _ in range(800)]
+        nodes = []
+        for r in range(4):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        w = torch.tensor([[0.5, 0.25, 0.0, 0.25], [0.25, 0.5, 0.25, 0.0],
+                          [0.0, 0.25, 0.5, 0.25], [0.25, 0.0, 0.25, 0.5]])
+        topo = {"edges": {0: [1, 3], 1: [0, 2], 2: [3, 1], 3: [2, 0]}, "weights": w,
+                "cliques": [[1, 0], [2, 3]]}
+        orig = d_sgd.gradient
+        if grad == "oracle":
+            def cpu_gradient(nds, t, p):
+                oracle_mod.reference_loop_clique_gradient(nds, t["cliques"])
+                for c in t["cliques"]:
+                    for r in c:
+                        nds[r]["optimizer"].step()
+            d_sgd.gradient = cpu_gradient
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for _ in range(5):
+                state, losses, done, active = d_sgd.next_step(state, params, None)
+        finally:
+            d_sgd.gradient = orig
+        return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
+                for n in nodes]
+
+    a = run("gpu")
+    b = run("oracle")
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 def test_consensus_distance_event(gpu, tmp_path):
     """The GPU consensus-distance event has the reference's schema and statistics."""
     from niidmix import logger as nl

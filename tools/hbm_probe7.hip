@@ -45,6 +45,40 @@ void rows(const float *__restrict__ x, float *__restrict__ y, long p, const int 
         }
 }
 
+// blocked layout [P/B][N][B]: item = (column block kb, clique, 1 KiB chunk inside the block)
+template <int WAVES, int RPW>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void rows_blocked(const float *__restrict__ x, float *__restrict__ y, long n, long bw, const int *__restrict__ members, int rpc, int n_cliques, long n_chunks) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long t = blockIdx.x;
+    const long xcd = t & 7, local = t >> 3;
+    const long chunk = (local / n_cliques) * 8 + xcd;       // global 256-column chunk
+    const int cq = (int)(local % n_cliques);
+    if (chunk >= n_chunks) return;
+    const long cpb = bw / 256, kb = chunk / cpb, cin = chunk % cpb;
+    const float *xc = x + kb * n * bw + cin * 256 + 4 * lane;
+    float *yc = y + kb * n * bw + cin * 256 + 4 * lane;
+    int myrow = 0;
+    if (lane < RPW && wave + WAVES * lane < rpc) myrow = members[cq * rpc + wave + WAVES * lane];
+    f4 v[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+        if (wave + WAVES * r < rpc) {
+            const long row = __builtin_amdgcn_readlane(myrow, r);
+            v[r] = __builtin_nontemporal_load((const f4 *)(xc + row * bw));
+        }
+    f4 s = v[0];
+#pragma unroll
+    for (int r = 1; r < RPW; ++r) s += v[r];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+        if (wave + WAVES * r < rpc) {
+            const long row = __builtin_amdgcn_readlane(myrow, r);
+            __builtin_nontemporal_store(v[r] + 1e-30f * s, (f4 *)(yc + row * bw));
+        }
+}
+
 __global__ void once(const f4 *__restrict__ x, f4 *__restrict__ y, long n4) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i < n4) __builtin_nontemporal_store(__builtin_nontemporal_load(x + i), y + i);
@@ -104,6 +138,53 @@ int main() {
     const long it1 = C * (((P / 256) + 7) / 8) * 8;
     const long n4 = N * P / 4;
     std::vector<void *> hold;
+    // fresh VMM pairs held alive (no chunk reuse), row-major vs blocked B=4096 on each
+    {
+        std::vector<VmmSlab> keep;
+        for (int k = 0; k < 8; ++k) {
+            VmmSlab sx, sy;
+            if (!vmm_alloc(sx, bytes, false, 0, 1) || !vmm_alloc(sy, bytes, false, 0, 1)) { printf("VMM allocation failed\n"); break; }
+            float *x = (float *)sx.va, *y = (float *)sy.va;
+            CK(hipMemset(x, 0, bytes)); CK(hipMemset(y, 0, bytes));
+            const float t0 = timeit([&] { rows<16, 7><<<it1, 1024>>>(x, y, P, dm, R, C, P / 256); });
+            const float t1 = timeit([&] { rows_blocked<16, 7><<<it1, 1024>>>(x, y, N, 4096, dm, R, C, P / 256); });
+            const float t2 = timeit([&] { rows_blocked<16, 7><<<it1, 1024>>>(x, y, N, 16384, dm, R, C, P / 256); });
+            printf("fresh VMM pair %d: row-major %.3f ms  blocked B=4096 %.3f ms  B=16384 %.3f ms\n", k, t0, t1, t2);
+            fflush(stdout);
+            keep.push_back(sx); keep.push_back(sy);
+        }
+        for (auto &v : keep) vmm_free(v);
+    }
+    // fresh hipMalloc pairs held alive
+    {
+        std::vector<float *> keep;
+        for (int k = 0; k < 6; ++k) {
+            float *x = nullptr, *y = nullptr;
+            CK(hipMalloc(&x, bytes)); CK(hipMalloc(&y, bytes));
+            CK(hipMemset(x, 0, bytes)); CK(hipMemset(y, 0, bytes));
+            const float t0 = timeit([&] { rows<16, 7><<<it1, 1024>>>(x, y, P, dm, R, C, P / 256); });
+            const float t1 = timeit([&] { rows_blocked<16, 7><<<it1, 1024>>>(x, y, N, 4096, dm, R, C, P / 256); });
+            printf("fresh hipMalloc pair %d: row-major %.3f ms  blocked B=4096 %.3f ms\n", k, t0, t1);
+            fflush(stdout);
+            keep.push_back(x); keep.push_back(y);
+        }
+        for (auto v : keep) CK(hipFree(v));
+    }
+    return 0;
+    // blocked layouts on physically contiguous slabs
+    {
+        float *x = nullptr, *y = nullptr;
+        if (hipExtMallocWithFlags((void **)&x, bytes, hipDeviceMallocContiguous) == hipSuccess &&
+            hipExtMallocWithFlags((void **)&y, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+            CK(hipMemset(x, 0, bytes)); CK(hipMemset(y, 0, bytes));
+            for (long bw : {1L << 20, 1L << 18, 1L << 16, 1L << 14, 1L << 12, 1L << 10}) {
+                const float tc = timeit([&] { rows_blocked<16, 7><<<it1, 1024>>>(x, y, N, bw, dm, R, C, P / 256); });
+                printf("contiguous, blocked layout B=%8ld: clique pattern %.3f ms\n", bw, tc);
+                fflush(stdout);
+            }
+            CK(hipFree(x)); CK(hipFree(y));
+        }
+    }
     // x and y inside ONE physically contiguous allocation, y = x + bytes + delta
     {
         const size_t extra = 64u << 20;
