@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="dcliques1000",
-                    choices=["dcliques1000", "ring100", "fc1000", "dcliques1000-smallworld"])
+                    choices=["dcliques1000", "ring100", "fc1000", "dcliques1000-smallworld",
+                             "dcliques10000"])
     ap.add_argument("--p", type=int, default=None, help="parameters per node (default per config)")
     ap.add_argument("--kernel", default="auto",
                     choices=["auto", "csr-exact", "csr-fast", "clique", "dense", "staged-exact", "staged-fast", "tile-exact", "tile-fast", "tile-lds-exact", "tile-lds-fast"])
@@ -83,6 +84,9 @@ def parse():
                     help="mix: the headline neighbour mixing round; grad-clique: the --clique-gradient "
                          "gradient mean (k_grad_segment_mean) over the same 1000-node d-cliques "
                          "topology (single GPU)")
+    ap.add_argument("--nodes-per-gpu", type=int, default=1000,
+                    help="multi-GPU weak scaling: nodes per rank (nodes x GPUs a multiple of 100; 1250 at "
+                         "--gpus 8 gives BASELINE configs[4], 10000 nodes)")
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
     return ap.parse_args()
@@ -111,6 +115,12 @@ def single_gpu_topology(cfg):
     if cfg == "ring100":
         csr, cl = golden("ring100_p257")
         return csr, cl, 62006, "ring N=100 (MH 1/3), P=62006 (LeNet-size)"
+    if cfg == "dcliques10000":
+        from niidmix.generate import dcliques_csr
+        csr, cl = dcliques_csr(10000, 100, "fully-connected", 1337)
+        return csr, cl, 1 << 20, ("d-cliques N=10000 (100 cliques x 100, fully-connected interclique, "
+                                  "MH; the reference's generator restated, seed 1337) on ONE GPU: "
+                                  "2 x 42 GB slabs resident in HBM")
     if cfg == "fc1000":
         n = 1000
         csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
@@ -308,28 +318,31 @@ def main():
         # torch's default allocator instead (placement-dependent speed, for comparison)
         alloc = (lambda: torch.empty(n_local, ld, device=dev)) if args.hipmalloc_slabs else \
             (lambda: memory.empty_slab(n_local, ld, dev))
-        xa = alloc()
-        xa.normal_(generator=gen)
-        xa = xa[:, :p]
-        xb = alloc()[:, :p]
-        halo = 0
-        k0 = args.kernel if args.kernel != "auto" else mixer.kernel_for("fast", xa)
+        k0 = args.kernel
+        if k0 == "auto":
+            k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
         if (args.layout == "blocked" and k0 == "clique" and args.workload == "mix"
-                and mixer.plan.max_clique <= 256):
+                and mixer.plan.max_clique <= 256 and not args.hipmalloc_slabs and p % 4 == 0):
             # device-resident node state in the column-blocked layout [K, N, 4096]
-            xa = memory.to_blocked(xa)
+            xa = memory.empty_blocked(n_local, p, dev)
+            xa.normal_(generator=gen)
             xb = memory.empty_blocked(n_local, p, dev)
-            torch.cuda.empty_cache()
+        else:
+            xa = alloc()
+            xa.normal_(generator=gen)
+            xa = xa[:, :p]
+            xb = alloc()[:, :p]
+        halo = 0
     else:
         from niidmix.shard import ShardedMixer
         p = args.p or (1 << 20)
-        mixer = ShardedMixer.dcliques(n_per_rank=1000, clique_size=100, world=world, rank=rank,
+        mixer = ShardedMixer.dcliques(n_per_rank=args.nodes_per_gpu, clique_size=100, world=world, rank=rank,
                                       interclique=args.interclique, device=dev, p=p,
                                       windows=args.windows)
         n_local, n_total = mixer.n_local, mixer.n_total
         halo = mixer.halo_rows
         desc = (f"d-cliques N={n_total} ({n_total // 100} cliques x 100, {args.interclique} "
-                f"interclique, MH), 1000 nodes per GPU; halo rows over RCCL")
+                f"interclique, MH), {args.nodes_per_gpu} nodes per GPU; halo rows over RCCL")
         parallelism = (f"{world} clique-aligned node shards, RCCL (xGMI) halo exchange pipelined "
                        f"over {mixer.k} column windows")
         csr = None
@@ -421,7 +434,7 @@ def main():
         if world == 1 and args.e2e:
             e2e = e2e_rounds(mixer, n_local, p, dev)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.config != "dcliques10000":
             if args.workload == "grad-clique":
                 cpu = cpu_baseline_grad(cliques, csr.n, p)
             else:

@@ -304,8 +304,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
     static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
-    // timing-only ablations (WRONG results; tools/tune_inproc.py): 4 = skip residual gathers,
-    // 8 = skip the cross-wave LDS reduction (per-wave group sums only, no barriers)
+    // timing-only ablations (WRONG results; instantiated only with -DNIIDMIX_ABLATIONS for
+    // tools/tune_inproc.py): 4 = skip residual gathers, 8 = skip the cross-wave LDS reduction
     constexpr bool NO_RES = (FL & 4) != 0, NO_RED = (FL & 8) != 0;
     constexpr bool PLAIN_ST = (FL & 16) != 0;   // write-back (L2) stores instead of non-temporal
     constexpr int RQ = 2;                     // residual rows per wave held in registers
@@ -1296,10 +1296,13 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 #define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s, bg)
     NIIDMIX_TILE(8, 2, 8, 64, 2, 4); NIIDMIX_TILE(8, 4, 8, 64, 2, 4); NIIDMIX_TILE(16, 4, 8, 64, 2, 4);
     NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
-    // tuning alternatives / timing-only ablations
+    // tuning alternatives (all exact-result variants; the timing-only ablations FL & 4 / FL & 8 are
+    // built only with -DNIIDMIX_ABLATIONS, never into the shipped library)
     NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 7, 8, 0, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 2, 4);
-    NIIDMIX_TILE(16, 7, 8, 64, 6, 4); NIIDMIX_TILE(16, 7, 8, 64, 10, 4); NIIDMIX_TILE(16, 7, 8, 64, 18, 4);
     NIIDMIX_TILE(16, 7, 8, 64, 16, 4);
+#ifdef NIIDMIX_ABLATIONS
+    NIIDMIX_TILE(16, 7, 8, 64, 6, 4); NIIDMIX_TILE(16, 7, 8, 64, 10, 4);
+#endif
 #undef NIIDMIX_TILE
     return set_error(NIIDMIX_EUNSUPPORTED, "no clique tile %dx%dx%dx%dx%dx%d", waves, rpw, occ, rw, ob, v);
 }

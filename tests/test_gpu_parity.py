@@ -321,3 +321,25 @@ def test_stream_copy(gpu):
         _lib.check(_lib.lib.niidmix_stream_copy_f32(a.data_ptr(), b.data_ptr(), n, s))
         torch.cuda.synchronize()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [3000, 10000])
+def test_clique_many_gateways(n, gpu, oracle_mod):
+    """Fully-connected interclique over many cliques: 29 / 99 gateway (residual) entries per
+    clique, i.e. the 128-entry descriptor path at 10 000 nodes; row-major and blocked slabs."""
+    from niidmix import memory, ops
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(n, 100, "fully-connected", 1337)
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.plan is not None, m.plan_reason
+    gen = torch.Generator().manual_seed(n)
+    xh = torch.randn(n, 256, generator=gen)
+    x = xh.to(gpu)
+    y = m(x, kernel="clique").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+    assert ok, worst
+    yb = memory.empty_blocked(n, 256, gpu)
+    m.mix_blocked(memory.to_blocked(x), yb, 256)
+    assert np.array_equal(memory.from_blocked(yb, 256).cpu().numpy(), y)
