@@ -74,7 +74,7 @@ def parse():
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
     ap.add_argument("--layout", default="blocked", choices=["blocked", "rowmajor"],
                     help="single GPU, clique kernel: device-resident slabs column-blocked "
-                         "[P/4096, N, 4096] (default) or row-major [N, P]")
+                         "[P/1024, N, 1024] (default) or row-major [N, P]")
     ap.add_argument("--hipmalloc-slabs", action="store_true",
                     help="single GPU: allocate the slabs with torch's default (hipMalloc) allocator "
                          "instead of the VMM-mapped slab pool")
@@ -323,7 +323,7 @@ def main():
             k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
         if (args.layout == "blocked" and k0 == "clique" and args.workload == "mix"
                 and mixer.plan.max_clique <= 256 and not args.hipmalloc_slabs and p % 4 == 0):
-            # device-resident node state in the column-blocked layout [K, N, 4096]
+            # device-resident node state in the column-blocked layout [K, N, 1024]
             xa = memory.empty_blocked(n_local, p, dev)
             xa.normal_(generator=gen)
             xb = memory.empty_blocked(n_local, p, dev)

@@ -162,7 +162,7 @@ int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  * floats and block strides block_stride_x / block_stride_y floats), element (r, c) at
  *   base + (c / block_cols) * block_stride + r * ld + c % block_cols.
  * block_cols: a power of two >= 256.  This is the layout niidmix keeps device-resident node state
- * in (block_cols = 4096): a clique's member rows then sit 16 KiB apart instead of P*4 bytes, which
+ * in (block_cols = 1024): a clique's member rows then sit 4 KiB apart instead of P*4 bytes, which
  * measured robust to the slab's physical placement.  Cliques of <= 256 members. */
 int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
                                    int64_t block_cols, int64_t block_stride_x,

@@ -49,7 +49,9 @@ def empty_slab(rows, cols, device, dtype=torch.float32):
         return torch.empty((rows, cols), dtype=dtype, device=device)
 
 
-BLOCK_COLS = 4096
+import os
+
+BLOCK_COLS = int(os.environ.get("NIIDMIX_BLOCK_COLS", 1024))   # power of two >= 256
 
 
 def empty_blocked(rows, p, device, block_cols=BLOCK_COLS):

@@ -45,7 +45,7 @@ def test_kernels_on_slab_memory_bitwise(gpu, oracle_mod):
 
 @pytest.mark.parametrize("p", [64, 4096, 10_000, 3 * 4096 + 256])
 def test_blocked_clique_equals_rowmajor(p, gpu, oracle_mod):
-    """The clique kernel on column-blocked slabs [K, N, 4096] gives bit-identical results to the
+    """The clique kernel on column-blocked slabs [K, N, B] gives bit-identical results to the
     row-major kernel (same arithmetic, different addresses), partial last block included."""
     from niidmix import memory, ops
     g = load_golden("dcliques1000_fc_p64")
