@@ -181,6 +181,44 @@ def e2e_rounds(mixer, n, p, dev, rounds=3):
     return res
 
 
+def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
+    """Host-resident drop-in round WITH gradient averaging (--clique-gradient): the fused device
+    round (niidmix.slab.FusedRoundRunner: H2D params + grads, gradient mean -> SGD step -> mixing,
+    D2H params) against the unfused one (gradient slab round trip, CPU-side nothing, then the
+    mixing slab round trip; the optimizer step itself is not timed there)."""
+    from niidmix import ops
+    from niidmix.slab import FusedRoundRunner, SlabMixer
+    hp = torch.empty((n, p), dtype=torch.float32, pin_memory=True)
+    hg = torch.empty((n, p), dtype=torch.float32, pin_memory=True)
+    hp.normal_()
+    hg.normal_()
+    mixer = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+    w = int(os.environ.get("NIIDMIX_WINDOW", 1 << 15))
+    fused = FusedRoundRunner(grad_op, plan.stepped, 0.1, mixer, n, p, dev, window=w)
+    res = {}
+    for mode in ("fast", "exact"):
+        fused.run(hp, hg, mode=mode)
+        ts = []
+        for _ in range(rounds):
+            fused.run(hp, hg, mode=mode, timing=True)
+            ts.append(fused.last_timing["round_s"])
+        res[f"fused_{mode}_round_ms"] = round(float(np.median(ts)) * 1e3, 2)
+    del fused
+    g_run = SlabMixer(grad_op, n, p, dev, window=w)
+    m_run = SlabMixer(mixer, n, p, dev, window=w)
+    g_run.mix(hg)
+    m_run.mix(hp, mode="exact")
+    ts = []
+    for _ in range(rounds):
+        t0 = time.perf_counter()
+        g_run.mix(hg)
+        m_run.mix(hp, mode="exact")
+        ts.append(time.perf_counter() - t0)
+    res["unfused_exact_round_ms"] = round(float(np.median(ts)) * 1e3, 2)
+    res["window_cols"] = w
+    return res
+
+
 def load_traffic(path, key):
     try:
         with open(path) as f:
@@ -431,7 +469,11 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}")}
         e2e = None
-        if world == 1 and args.e2e:
+        if world == 1 and args.e2e and args.workload == "grad-clique":
+            del xa, xb
+            torch.cuda.empty_cache()
+            e2e = e2e_fused_rounds(mixer, plan, csr, cliques, n_local, p, dev)
+        elif world == 1 and args.e2e:
             e2e = e2e_rounds(mixer, n_local, p, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config != "dcliques10000":

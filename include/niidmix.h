@@ -263,6 +263,16 @@ int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_
                                   int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
                                   void *stream);
 
+/* SGD step on the listed rows: p[row] = fma(neg_lr, g[row], p[row]) — torch.optim.SGD with
+ * momentum 0 and no weight decay (param.add_(grad, alpha=-lr); ATen's CPU kernel fuses it into one
+ * fma with an fp32 alpha), the optimizer step the reference runs after gradient averaging
+ * (d_sgd.py:63-64, :77-78, :88-90).  The fused drop-in round (niidmix.d_sgd) runs gradient mean ->
+ * this step -> mixing on each device window, so the step never visits the host.
+ *   p [*, ld_p] parameters (device, updated in place), g [*, ld_g] gradients (device)
+ *   rows [n_rows] int32 rows to step (device) */
+int niidmix_sgd_step_rows_f32(float *p, int64_t ld_p, const float *g, int64_t ld_g, int64_t ncols,
+                              const int32_t *rows, int64_t n_rows, float neg_lr, void *stream);
+
 /* Device memory for node-state slabs, with the signatures of a PyTorch pluggable allocator
  * (torch.cuda.memory.CUDAPluggableAllocator; niidmix.memory.slab_pool uses them for a MemPool).
  * The range is reserved with hipMemAddressReserve and mapped from 2 MiB physical chunks

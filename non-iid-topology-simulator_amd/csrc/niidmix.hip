@@ -1223,6 +1223,30 @@ __global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restri
     }
 }
 
+// ----------------------------------------------------------------------------------------------
+// SGD step on listed rows (torch.optim.SGD, momentum 0, no weight decay: param.add_(grad,
+// alpha=-lr), whose ATen CPU kernel computes fma(-lr, g, p) with fp32 alpha — one rounding):
+//   p[row] = fma(neg_lr, g[row], p[row])    for row in rows
+// The fused drop-in round runs it between the gradient mean and the mixing, on device windows.
+template <int V>
+__global__ __launch_bounds__(256) void k_sgd_step_rows(float *__restrict__ p, int64_t ld_p,
+                                                       const float *__restrict__ g, int64_t ld_g,
+                                                       int64_t ncols, const int32_t *__restrict__ rows,
+                                                       int64_t n_rows, float neg_lr, int64_t n_chunks) {
+    for (int64_t t = blockIdx.x; t < n_rows * n_chunks; t += gridDim.x) {
+        const int64_t r = rows[t / n_chunks];
+        const int64_t c = (t % n_chunks) * (256 * V) + (int64_t)threadIdx.x * V;
+        if (c >= ncols) continue;
+        float pv[V], gv[V];
+        ldv<V>(p + r * ld_p + c, pv);
+        ldv<V>(g + r * ld_g + c, gv);
+#pragma unroll
+        for (int e = 0; e < V; ++e) pv[e] = __builtin_fmaf(neg_lr, gv[e], pv[e]);
+        if constexpr (V == 4) *reinterpret_cast<float4 *>(p + r * ld_p + c) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+        else p[r * ld_p + c] = pv[0];
+    }
+}
+
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int64_t grid_for(int64_t items) { return items < kMaxGrid ? ((items + 7) / 8) * 8 : kMaxGrid; }
@@ -1719,6 +1743,25 @@ int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_
         hipLaunchKernelGGL((k_grad_segment_mean<1, 16>), grid, block, 0, s, g, ld_g, y, ld_y, p, n_seg,
                            seg_ptr, seg_row, n_chunks);
     return check_launch("k_grad_segment_mean");
+}
+
+int niidmix_sgd_step_rows_f32(float *p, int64_t ld_p, const float *g, int64_t ld_g, int64_t ncols,
+                              const int32_t *rows, int64_t n_rows, float neg_lr, void *stream) {
+    if (ncols < 0 || n_rows < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (ncols == 0 || n_rows == 0) return NIIDMIX_OK;
+    if (!p || !g || !rows) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_p < ncols || ld_g < ncols) return set_error(NIIDMIX_EINVAL, "leading dimension < ncols");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool vec4 = ncols % 4 == 0 && ld_p % 4 == 0 && ld_g % 4 == 0 && aligned16(p) && aligned16(g);
+    const int64_t cols = vec4 ? 1024 : 256;
+    const int64_t n_chunks = (ncols + cols - 1) / cols;
+    const int64_t items = n_rows * n_chunks;
+    const dim3 grid((unsigned)(items < kMaxGrid ? items : kMaxGrid)), block(256);
+    if (vec4)
+        hipLaunchKernelGGL(k_sgd_step_rows<4>, grid, block, 0, s, p, ld_p, g, ld_g, ncols, rows, n_rows, neg_lr, n_chunks);
+    else
+        hipLaunchKernelGGL(k_sgd_step_rows<1>, grid, block, 0, s, p, ld_p, g, ld_g, ncols, rows, n_rows, neg_lr, n_chunks);
+    return check_launch("k_sgd_step_rows");
 }
 
 int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,

@@ -133,6 +133,65 @@ def gradient(nodes, topology, params):
         nodes[r]["optimizer"].step()
 
 
+def _fused_ok(params):
+    """The fused device round applies when gradients are averaged and the optimizer step is plain
+    SGD (momentum 0: the reference's default, d_sgd.py:262-263); NIIDMIX_FUSED=0 disables it."""
+    alg = params["algorithm"]
+    return (_averages_gradients(params) and float(alg.get("learning-momentum", 0.0)) == 0.0
+            and os.environ.get("NIIDMIX_FUSED", "1") != "0")
+
+
+class _FusedEngine:
+    """Parameter slab + gradient slab + GradMean + Mixer + FusedRoundRunner."""
+
+    def __init__(self, nodes, topology, params, device):
+        from .gradient import GradMean, build_grad_plan
+        from .ops import Mixer
+        from .slab import FusedRoundRunner, NodeSlab
+        self.topology = topology
+        self.weights_id = id(topology.get("weights"))
+        self.key = _grad_key(params) + (float(params["algorithm"]["learning-rate"]),)
+        models = [n["model"] for n in nodes]
+        self.slab = NodeSlab(models)
+        self.gslab = NodeSlab(models, grads=True)
+        self.plan = build_grad_plan(len(nodes), topology, params)
+        csr = to_csr(topology)
+        if csr.n != self.slab.n:
+            raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=device)
+        self.runner = FusedRoundRunner(GradMean(self.plan, device), self.plan.stepped,
+                                       params["algorithm"]["learning-rate"], self.mixer,
+                                       self.slab.n, self.slab.p, device,
+                                       window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
+
+    def valid_for(self, nodes, topology, params):
+        models = [n["model"] for n in nodes]
+        return (topology is self.topology and id(topology.get("weights")) == self.weights_id
+                and _grad_key(params) + (float(params["algorithm"]["learning-rate"]),) == self.key
+                and self.slab.owns(models) and self.gslab.owns(models))
+
+
+_fused_engines = {}
+
+
+def fused_round(nodes, topology, params):
+    """gradient(nodes, topology, params) followed by average(nodes, topology, params), as one
+    device round: gradient mean, SGD step and mixing on each column window, one H2D of parameters
+    and gradients and one D2H of the mixed parameters (niidmix.slab.FusedRoundRunner)."""
+    key = id(nodes)
+    eng = _fused_engines.get(key)
+    if eng is None or not eng.valid_for(nodes, topology, params):
+        dev = torch.device("cuda", torch.cuda.current_device())
+        eng = _FusedEngine(nodes, topology, params, dev)
+        _fused_engines.clear()
+        _fused_engines[key] = eng
+    logging.info("  fused gradient %s + SGD step + mixing (GPU, %s)", eng.plan.kind, _mode(params))
+    eng.runner.run(eng.slab.host, eng.gslab.host, mode=_mode(params),
+                   timing=logging.getLogger().isEnabledFor(logging.INFO))
+    if eng.runner.last_timing:
+        logging.info("  fused round: %s", eng.runner.last_timing)
+
+
 # ------------------------------------------------------------------------------------------------
 # the GPU mixing step
 class _Engine:
@@ -261,8 +320,11 @@ def next_step(state, params, rundir):
             node["train-iterator"] = rest
         epoch_done[node["rank"]] = done
     if not sample:
-        gradient(active, topology, params)
-        average(active, topology, params)                 # ★ GPU
+        if _fused_ok(params):
+            fused_round(active, topology, params)         # ★ GPU: gradient + step + mixing
+        else:
+            gradient(active, topology, params)
+            average(active, topology, params)             # ★ GPU
         if params["topology"]["name"] == "random-graph" and params["topology"]["randomize"]:
             params["topology"]["topology-seed"] += 1
             from setup.topology.random_graph import generate_topology   # reference generator

@@ -9,6 +9,7 @@ Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
   grad_segment_mean(g, seg_ptr, seg_row, out)       k_grad_segment_mean (clique gradient mean)
+  sgd_step_rows(p, g, rows, neg_lr)                 k_sgd_step_rows (the optimizer step, fused round)
   mix_csr(..., mode | MEAN)                         per-row gradient mean (unbiased / removed edges)
 All ops launch on torch's current HIP stream of the input's device, never synchronise, and raise
 RuntimeError (TORCH_CHECK-style) on bad arguments.  They accept HIP tensors only: there is no CPU
@@ -283,6 +284,18 @@ def grad_segment_mean(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: torch.Ten
                                                 g.shape[1], seg_ptr.numel() - 1,
                                                 seg_ptr.data_ptr(), seg_row.data_ptr(), _stream(g))
     _lib.check(rc, "niidmix::grad_segment_mean")
+
+
+@torch.library.custom_op("niidmix::sgd_step_rows", mutates_args=("p",))
+def sgd_step_rows(p: torch.Tensor, g: torch.Tensor, rows: torch.Tensor, neg_lr: float) -> None:
+    """p[rows] = fma(neg_lr, g[rows], p[rows]) in place (torch.optim.SGD, momentum 0)."""
+    _slab("p", p)
+    _slab("g", g, rows=p.shape[0], cols=p.shape[1])
+    _req(g.device == p.device, "p and g must be on the same device")
+    _vec("rows", rows, torch.int32, p.device)
+    rc = _lib.lib.niidmix_sgd_step_rows_f32(p.data_ptr(), _ld(p), g.data_ptr(), _ld(g), p.shape[1],
+                                            rows.data_ptr(), rows.numel(), float(neg_lr), _stream(p))
+    _lib.check(rc, "niidmix::sgd_step_rows")
 
 
 # ------------------------------------------------------------------------------------------------

@@ -153,3 +153,75 @@ class SlabMixer:
                                 "gpu_span_s": t_ev[0].elapsed_time(t_ev[1]) / 1e3,
                                 "windows": nwin, "window_cols": w}
         return host
+
+
+class FusedRoundRunner:
+    """One drop-in round with gradient averaging, fused on the device:
+    per column window, H2D of the parameter AND gradient slabs, then on the device
+        gradient mean (GradMean)  ->  SGD step on the stepped rows  ->  mixing (Mixer)
+    and D2H of the mixed parameters only.  The reference's equivalent is d_sgd.gradient (CPU mean
+    + optimizer.step on every stepped node) followed by d_sgd.average; per window the arithmetic is
+    the same, bit for bit, and columns are independent, so windows pipeline as in SlabMixer.
+    The host gradients keep the nodes' own gradients (the reference leaves the averaged ones
+    there until the next zero_grad; nothing reads them in between)."""
+
+    def __init__(self, grad_op, step_rows, lr, mixer, n, p, device, window=1 << 15):
+        self.grad_op = grad_op
+        self.mixer = mixer
+        self.n, self.p = n, p
+        self.device = torch.device(device)
+        self.neg_lr = -float(lr)
+        self.rows = torch.as_tensor(step_rows, dtype=torch.int32).to(self.device)
+        self.window = max(256, (min(window, p) + 255) // 256 * 256)
+        w = self.window
+        mk = lambda: torch.empty((n, w), dtype=torch.float32, device=self.device)  # noqa: E731
+        self.dp = [mk(), mk()]
+        self.dg = [mk(), mk()]
+        self.dy = [mk(), mk()]
+        self.dm = mk()
+        self.s_h2d = torch.cuda.Stream(self.device)
+        self.s_mix = torch.cuda.Stream(self.device)
+        self.s_d2h = torch.cuda.Stream(self.device)
+        self.last_timing = None
+
+    def run(self, host_params, host_grads, mode="exact", timing=False):
+        from . import ops
+        n, p, w = self.n, self.p, self.window
+        for h in (host_params, host_grads):
+            assert h.shape == (n, p) and h.dtype == torch.float32 and h.stride(1) == 1
+        ld_p, ld_g = host_params.stride(0) * 4, host_grads.stride(0) * 4
+        bp, bg = host_params.data_ptr(), host_grads.data_ptr()
+        nwin = (p + w - 1) // w
+        ev_in = [torch.cuda.Event() for _ in range(nwin)]
+        ev_mix = [torch.cuda.Event() for _ in range(nwin)]
+        ev_out = [torch.cuda.Event() for _ in range(nwin)]
+        t0 = time.perf_counter()
+        for k in range(nwin):
+            c0 = k * w
+            cw = min(w, p - c0)
+            buf = k % 2
+            with torch.cuda.stream(self.s_h2d):
+                if k >= 2:
+                    self.s_h2d.wait_event(ev_mix[k - 2])
+                _copy2d(self.dp[buf].data_ptr(), w * 4, bp + c0 * 4, ld_p, cw * 4, n, 0, self.s_h2d)
+                _copy2d(self.dg[buf].data_ptr(), w * 4, bg + c0 * 4, ld_g, cw * 4, n, 0, self.s_h2d)
+                ev_in[k].record(self.s_h2d)
+            with torch.cuda.stream(self.s_mix):
+                self.s_mix.wait_event(ev_in[k])
+                if k >= 2:
+                    self.s_mix.wait_event(ev_out[k - 2])
+                xp, xg, gm = self.dp[buf][:, :cw], self.dg[buf][:, :cw], self.dm[:, :cw]
+                self.grad_op(xg, out=gm)
+                if self.rows.numel():
+                    ops.sgd_step_rows(xp, gm, self.rows, self.neg_lr)
+                self.mixer(xp, out=self.dy[buf][:, :cw], mode=mode)
+                ev_mix[k].record(self.s_mix)
+            with torch.cuda.stream(self.s_d2h):
+                self.s_d2h.wait_event(ev_mix[k])
+                _copy2d(bp + c0 * 4, ld_p, self.dy[buf].data_ptr(), w * 4, cw * 4, n, 1, self.s_d2h)
+                ev_out[k].record(self.s_d2h)
+        self.s_d2h.synchronize()
+        if timing:
+            self.last_timing = {"round_s": time.perf_counter() - t0, "windows": nwin,
+                                "window_cols": w}
+        return host_params

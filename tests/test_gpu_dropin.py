@@ -158,19 +158,37 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
         assert torch.equal(u, v)
 
 
-def test_training_rounds_clique_gradient(gpu, oracle_mod):
-    """Rounds with --clique-gradient (2 cliques of 2, linear model): the drop-in's GPU gradient
-    averaging through the pinned gradient slab (kept across rounds by in-place zero_grad) gives
-    the same parameters, bit for bit, as the reference's CPU clique-gradient loop."""
+@pytest.mark.parametrize("alg", ["clique", "unbiased"])
+def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
+    """Rounds with --clique-gradient / --unbiased-gradient (linear model, 4 nodes): the drop-in's
+    fused device round (gradient mean + SGD step + mixing) and its unfused GPU path (gradient
+    slab, then the mixing slab) give the same parameters, bit for bit, as the reference's CPU
+    loops (average_gradients / update_gradients / optimizer.step, then the reference mixing loop)."""
     from niidmix import d_sgd
 
-    def run(grad):
+    def cpu_gradient(nds, t, p):                  # d_sgd.py:47-94 restated with torch CPU ops
+        with torch.no_grad():
+            if p["algorithm"]["clique-gradient"]:
+                oracle_mod.reference_loop_clique_gradient(nds, t["cliques"])
+                stepped = [r for c in t["cliques"] for r in c]
+            else:
+                hoods = t["neighbourhoods"]
+                grads = {n["rank"]: d_sgd.average_gradients([nds[q]["model"] for q in hoods[n["rank"]]])
+                         for n in nds}
+                for n in nds:
+                    d_sgd.update_gradients([n["model"]], grads[n["rank"]])
+                stepped = [n["rank"] for n in nds]
+        for r in stepped:
+            nds[r]["optimizer"].step()
+
+    def run(path):
+        monkeypatch.setenv("NIIDMIX_FUSED", "1" if path == "fused" else "0")
         torch.manual_seed(1337)
         params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
                   "topology": {"name": "d-cliques", "remove-clique-edges": 0},
                   "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 50,
-                                "initial-averaging": False, "clique-gradient": True,
-                                "unbiased-gradient": False}}
+                                "initial-averaging": False, "clique-gradient": alg == "clique",
+                                "unbiased-gradient": alg == "unbiased"}}
 
         class Net(torch.nn.Module):
             def __init__(self):
@@ -191,28 +209,44 @@ def test_training_rounds_clique_gradient(gpu, oracle_mod):
         w = torch.tensor([[0.5, 0.25, 0.0, 0.25], [0.25, 0.5, 0.25, 0.0],
                           [0.0, 0.25, 0.5, 0.25], [0.25, 0.0, 0.25, 0.5]])
         topo = {"edges": {0: [1, 3], 1: [0, 2], 2: [3, 1], 3: [2, 0]}, "weights": w,
-                "cliques": [[1, 0], [2, 3]]}
-        orig = d_sgd.gradient
-        if grad == "oracle":
-            def cpu_gradient(nds, t, p):
-                oracle_mod.reference_loop_clique_gradient(nds, t["cliques"])
-                for c in t["cliques"]:
-                    for r in c:
-                        nds[r]["optimizer"].step()
+                "cliques": [[1, 0], [2, 3]],
+                "neighbourhoods": {0: [0, 2], 1: [3, 1, 0], 2: [2], 3: [1, 3]}}
+        orig_g, orig_a = d_sgd.gradient, d_sgd.average
+        if path == "oracle":
             d_sgd.gradient = cpu_gradient
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
         try:
             state, _, _ = d_sgd.init(nodes, topo, params)
             for _ in range(5):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
         finally:
-            d_sgd.gradient = orig
+            d_sgd.gradient, d_sgd.average = orig_g, orig_a
         return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
                 for n in nodes]
 
-    a = run("gpu")
-    b = run("oracle")
-    for u, v in zip(a, b):
-        assert torch.equal(u, v)
+    fused, unfused, ref = run("fused"), run("unfused"), run("oracle")
+    for u, v, r in zip(fused, unfused, ref):
+        assert torch.equal(v, r)
+        assert torch.equal(u, r)
+
+
+def test_sgd_step_rows_matches_torch_cpu_sgd(gpu):
+    """k_sgd_step_rows == torch.optim.SGD(momentum=0).step on the CPU, bit for bit (ATen's CPU
+    add_(g, alpha=-lr) is one fma with an fp32 alpha), on the listed rows only."""
+    from niidmix import ops
+    gen = torch.Generator().manual_seed(5)
+    p = torch.randn(6, 1003, generator=gen)
+    g = torch.randn(6, 1003, generator=gen)
+    rows = [0, 2, 5]
+    ref = p.clone()
+    for r in rows:
+        q = torch.nn.Parameter(ref[r].clone())
+        q.grad = g[r].clone()
+        torch.optim.SGD([q], lr=0.07).step()
+        ref[r] = q.detach()
+    pd = p.to(gpu)
+    ops.sgd_step_rows(pd, g.to(gpu), torch.tensor(rows, dtype=torch.int32, device=gpu), -0.07)
+    assert torch.equal(pd.cpu(), ref)
 
 
 def test_consensus_distance_event(gpu, tmp_path):
