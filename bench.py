@@ -359,8 +359,9 @@ def main():
         k0 = args.kernel
         if k0 == "auto":
             k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
-        if (args.layout == "blocked" and k0 == "clique" and args.workload == "mix"
-                and mixer.plan.max_clique <= 256 and not args.hipmalloc_slabs and p % 4 == 0):
+        if (args.layout == "blocked" and not args.hipmalloc_slabs and p % 4 == 0 and
+                ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 256) or
+                 args.workload == "grad-clique")):
             # device-resident node state in the column-blocked layout [K, N, 1024]
             xa = memory.empty_blocked(n_local, p, dev)
             xa.normal_(generator=gen)
@@ -392,14 +393,16 @@ def main():
     mode = "exact" if kernel.endswith("exact") else "fast"
 
     blocked = world == 1 and xa.dim() == 3
-    if blocked:
+    if blocked and args.workload == "mix":
         kernel = "clique"
 
     def step(a, b, evs=None):
         if world == 1:
             if evs is not None:
                 evs[0].record(torch.cuda.current_stream(dev))
-            if blocked:
+            if blocked and args.workload == "grad-clique":
+                mixer.mean_blocked(a, b, p)
+            elif blocked:
                 mixer.mix_blocked(a, b, p)
             else:
                 mixer(a, out=b, kernel=kernel, mode=mode)

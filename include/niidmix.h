@@ -263,6 +263,14 @@ int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_
                                   int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
                                   void *stream);
 
+/* niidmix_grad_segment_mean_f32 on column-blocked slabs [K][rows][block_cols] (see
+ * niidmix_mix_clique_blocked_f32; block_cols a power of two >= 1024, p % 4 == 0). */
+int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t p, int64_t ld,
+                                          int64_t block_cols, int64_t block_stride_g,
+                                          int64_t block_stride_y, int64_t n_seg,
+                                          const int32_t *seg_ptr, const int32_t *seg_row,
+                                          void *stream);
+
 /* SGD step on the listed rows: p[row] = fma(neg_lr, g[row], p[row]) — torch.optim.SGD with
  * momentum 0 and no weight decay (param.add_(grad, alpha=-lr); ATen's CPU kernel fuses it into one
  * fma with an fp32 alpha), the optimizer step the reference runs after gradient averaging

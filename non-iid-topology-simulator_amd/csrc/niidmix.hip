@@ -1177,13 +1177,21 @@ __global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restri
                                                            int64_t p, int64_t n_seg,
                                                            const int32_t *__restrict__ seg_ptr,
                                                            const int32_t *__restrict__ seg_row,
-                                                           int64_t n_chunks) {
+                                                           int64_t n_chunks, int cpb_shift,
+                                                           int64_t bs_g, int64_t bs_y) {
+    // column-blocked slabs: chunk k (256*V columns) lives in block k >> cpb_shift, block strides
+    // bs_g / bs_y floats (row-major: cpb_shift = 62, one block)
     const int lane = threadIdx.x & (kWave - 1);
     for (int64_t t = blockIdx.x; t < n_seg * n_chunks; t += gridDim.x) {
         const int64_t seg = t / n_chunks;
-        const int64_t c = (t % n_chunks) * (256 * V) + (int64_t)threadIdx.x * V;
+        const int64_t chunk = t % n_chunks;
+        const int64_t kb = chunk >> cpb_shift;
+        const int64_t cin = (chunk - (kb << cpb_shift)) * (256 * V) + (int64_t)threadIdx.x * V;
+        const int64_t c = chunk * (256 * V) + (int64_t)threadIdx.x * V;   // global column
         const bool ok = c < p;                   // p % V == 0: a thread is all-in or all-out
-        const int64_t cc = ok ? c : 0;           // loads stay unconditional
+        const int64_t cc = ok ? cin : 0;         // loads stay unconditional
+        const float *gb = g + kb * bs_g;
+        float *yb = y + kb * bs_y;
         const int beg = seg_ptr[seg], end = seg_ptr[seg + 1];
         float acc[V];
 #pragma unroll
@@ -1196,7 +1204,7 @@ __global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restri
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int jj = j + u < cnt ? j + u : cnt - 1;
-                    ldv<V>(g + (int64_t)__builtin_amdgcn_readlane(d_row, jj) * ld_g + cc, v[u]);
+                    ldv<V>(gb + (int64_t)__builtin_amdgcn_readlane(d_row, jj) * ld_g + cc, v[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
@@ -1216,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restri
             const int cnt = end - kb < 64 ? end - kb : 64;
             const int d_row = seg_row[kb + (lane < cnt ? lane : cnt - 1)];
             for (int j = 0; j < cnt; ++j) {
-                float *dst = y + (int64_t)__builtin_amdgcn_readlane(d_row, j) * ld_y + c;
+                float *dst = yb + (int64_t)__builtin_amdgcn_readlane(d_row, j) * ld_y + cin;
                 if (ok) stv_nt<V>(dst, o);
             }
         }
@@ -1738,10 +1746,35 @@ int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_
     const dim3 grid((unsigned)(n_items < kMaxGrid ? n_items : kMaxGrid)), block(256);
     if (vec4)
         hipLaunchKernelGGL((k_grad_segment_mean<4, 8>), grid, block, 0, s, g, ld_g, y, ld_y, p, n_seg,
-                           seg_ptr, seg_row, n_chunks);
+                           seg_ptr, seg_row, n_chunks, 62, (int64_t)0, (int64_t)0);
     else
         hipLaunchKernelGGL((k_grad_segment_mean<1, 16>), grid, block, 0, s, g, ld_g, y, ld_y, p, n_seg,
-                           seg_ptr, seg_row, n_chunks);
+                           seg_ptr, seg_row, n_chunks, 62, (int64_t)0, (int64_t)0);
+    return check_launch("k_grad_segment_mean");
+}
+
+int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t p, int64_t ld,
+                                          int64_t block_cols, int64_t block_stride_g,
+                                          int64_t block_stride_y, int64_t n_seg,
+                                          const int32_t *seg_ptr, const int32_t *seg_row,
+                                          void *stream) {
+    if (p < 0 || n_seg < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n_seg == 0 || p == 0) return NIIDMIX_OK;
+    if (!g || !y || !seg_ptr || !seg_row) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (block_cols < 1024 || (block_cols & (block_cols - 1)))
+        return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= 1024", (long long)block_cols);
+    if (ld < block_cols || block_stride_g < ld || block_stride_y < ld)
+        return set_error(NIIDMIX_EINVAL, "row stride < block_cols or block stride < row stride");
+    if (g == y) return set_error(NIIDMIX_EALIAS, "g and y alias: the mean is out-of-place");
+    if (p % 4 || ld % 4 || block_stride_g % 4 || block_stride_y % 4 || !aligned16(g) || !aligned16(y))
+        return set_error(NIIDMIX_EUNSUPPORTED, "blocked gradient mean needs p, strides % 4 == 0 and 16-B aligned slabs");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n_chunks = (p + 1023) / 1024;
+    const int64_t n_items = n_seg * n_chunks;
+    const dim3 grid((unsigned)(n_items < kMaxGrid ? n_items : kMaxGrid)), block(256);
+    const int shift = __builtin_ctzll((unsigned long long)(block_cols / 1024));
+    hipLaunchKernelGGL((k_grad_segment_mean<4, 8>), grid, block, 0, s, g, ld, y, ld, p, n_seg, seg_ptr,
+                       seg_row, n_chunks, shift, block_stride_g, block_stride_y);
     return check_launch("k_grad_segment_mean");
 }
 

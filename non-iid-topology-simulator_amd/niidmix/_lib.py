@@ -69,6 +69,8 @@ SIGNATURES = {
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp,
                                                      _vp]),
+    "niidmix_grad_segment_mean_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64,
+                                                             _i64, _i64, _vp, _vp, _vp]),
     "niidmix_sgd_step_rows_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _vp, _i64,
                                                  ctypes.c_float, _vp]),
     "niidmix_hbm_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, _vp]),

@@ -115,6 +115,13 @@ class GradMean:
             self.val = torch.ones(len(plan.col), dtype=torch.float32, device=dev)
             self.hint = self.ops.LOW_DEGREE if len(plan.col) <= 4 * max(self.n, 1) else 0
 
+    def mean_blocked(self, g, out, p):
+        """Segment mean on column-blocked slabs [K, rows, B] (device-resident layout)."""
+        if self.plan.seg_ptr is None:
+            raise RuntimeError("blocked slabs: only the clique-gradient segment mean")
+        self.ops.grad_segment_mean_blocked(g, self.seg_ptr, self.seg_row, out, int(p))
+        return out
+
     def __call__(self, g, out=None, mode=None, kernel=None):
         """mode / kernel are accepted for SlabMixer compatibility: the mean is exact in every mode
         (w = 1: fma(1, g, acc) == fl(acc + g))."""

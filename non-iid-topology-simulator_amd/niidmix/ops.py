@@ -286,6 +286,26 @@ def grad_segment_mean(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: torch.Ten
     _lib.check(rc, "niidmix::grad_segment_mean")
 
 
+@torch.library.custom_op("niidmix::grad_segment_mean_blocked", mutates_args=("out",))
+def grad_segment_mean_blocked(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: torch.Tensor,
+                              out: torch.Tensor, p: int) -> None:
+    """grad_segment_mean on column-blocked slabs g, out: [K, rows, B] (niidmix.memory)."""
+    for name, t in (("g", g), ("out", out)):
+        _req(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and
+             t.dim() == 3 and t.stride(2) == 1,
+             f"{name}: expected a HIP fp32 [K, rows, B] blocked slab with unit column stride")
+    _req(g.shape == out.shape and g.stride(1) == out.stride(1), "g and out: same blocked geometry")
+    k, rows, b = g.shape
+    _req(0 <= p <= k * b and (k == 0 or p > (k - 1) * b), f"p={p} does not fit {k} blocks of {b}")
+    _vec("seg_ptr", seg_ptr, torch.int32, g.device)
+    _vec("seg_row", seg_row, torch.int32, g.device)
+    _req(g.data_ptr() != out.data_ptr(), "g and out overlap: the mean is out-of-place")
+    rc = _lib.lib.niidmix_grad_segment_mean_blocked_f32(
+        g.data_ptr(), out.data_ptr(), int(p), g.stride(1), b, g.stride(0), out.stride(0),
+        seg_ptr.numel() - 1, seg_ptr.data_ptr(), seg_row.data_ptr(), _stream(g))
+    _lib.check(rc, "niidmix::grad_segment_mean_blocked")
+
+
 @torch.library.custom_op("niidmix::sgd_step_rows", mutates_args=("p",))
 def sgd_step_rows(p: torch.Tensor, g: torch.Tensor, rows: torch.Tensor, neg_lr: float) -> None:
     """p[rows] = fma(neg_lr, g[rows], p[rows]) in place (torch.optim.SGD, momentum 0)."""

@@ -74,6 +74,13 @@ def test_argument_errors_without_gpu():
     assert L.niidmix_grad_segment_mean_f32(16, 4, 16, 4, 4, 1, 8, 8, None) == _lib.EALIAS
     assert L.niidmix_grad_segment_mean_f32(16, 2, 1024, 4, 4, 1, 8, 8, None) == _lib.EINVAL
     assert L.niidmix_grad_segment_mean_f32(16, 4, 1024, 4, 4, 0, 8, 8, None) == _lib.OK
+    B = L.niidmix_grad_segment_mean_blocked_f32
+    assert B(None, 1024, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL    # null
+    assert B(16, 1024, 4, 1024, 1000, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL      # block_cols
+    assert B(16, 1024, 4, 1024, 1024, 512, 4096, 1, 8, 8, None) == _lib.EINVAL       # stride
+    assert B(16, 16, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EALIAS
+    assert B(16, 1024, 6, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EUNSUPPORTED  # p % 4
+    assert B(16, 1024, 4, 1024, 1024, 4096, 4096, 0, 8, 8, None) == _lib.OK         # empty
     rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
     assert rc == _lib.EINVAL
     assert L.niidmix_stream_copy_f32(16, 1024, 6, None) == _lib.EUNSUPPORTED   # n % 4

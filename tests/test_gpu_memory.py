@@ -66,3 +66,28 @@ def test_blocked_clique_equals_rowmajor(p, gpu, oracle_mod):
         ok, worst = oracle_mod.check_tolerance(memory.from_blocked(yb, 64).cpu().numpy(), g["y"],
                                                bound, rtol=1e-5)
         assert ok, worst
+
+
+@pytest.mark.parametrize("p", [64, 10_000, 3 * 4096 + 256])
+def test_blocked_grad_mean_equals_rowmajor(p, gpu, oracle_mod):
+    """The clique-gradient segment mean on column-blocked slabs is bit-identical to the row-major
+    kernel, and at p=64 to the reference's own averaged gradients (average_gradients,
+    d_sgd.py:19-27)."""
+    from conftest import load_grad
+    from niidmix import gradient, memory
+    d, topo, params = load_grad("grad_dcliques1000_fc_p64")
+    plan = gradient.build_grad_plan(d["g"].shape[0], topo, params)
+    gm = gradient.GradMean(plan, gpu)
+    if p == 64:
+        x = torch.from_numpy(d["g"]).to(gpu)
+    else:
+        x = torch.randn(plan.n, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(p))
+    y_ref = gm(x)
+    yb = memory.empty_blocked(plan.n, p, gpu)
+    gm.mean_blocked(memory.to_blocked(x), yb, p)
+    y = memory.from_blocked(yb, p)
+    assert torch.equal(y, y_ref)
+    if p == 64:
+        stepped = np.zeros(plan.n, bool)
+        stepped[plan.stepped] = True
+        assert oracle_mod.bitwise_equal(y.cpu().numpy()[stepped], d["g_out"][stepped])
