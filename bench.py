@@ -21,9 +21,12 @@ cpu_baseline (rank 0, N=1): the reference loop restated faithfully in torch CPU
 (oracle.reference_loop_average: per-node deepcopy / mul_(0) / add_(w*p), then update_models) timed
 on this host's cores for one full round of the same topology at the same P.
 
-Multi-GPU (N > 1): weak scaling, each rank owns 1000 nodes (10 cliques of 100); the global topology
-is d-cliques over 1000*N nodes (see --interclique), cliques sharded whole across ranks, and the
-cross-shard edges' rows are exchanged over RCCL (xGMI) every round before the mixing kernel.
+Multi-GPU (N > 1): weak scaling over a d-cliques topology of 1000*N nodes (see --interclique).
+--shard stripes (default): rank r mixes parameter columns [c0, c1) of EVERY node (P/N columns each,
+block-aligned; the round is independent per column), so per-rank bytes equal the N=1 round's and
+there is no data-path collective (niidmix.shard.StripedMixer).  --shard nodes: each rank owns 1000
+nodes (whole cliques) and the cross-shard edges' rows are exchanged over RCCL (xGMI) every round
+before the mixing kernel (niidmix.shard.ShardedMixer).
 """
 import argparse
 import ctypes
@@ -87,6 +90,9 @@ def parse():
     ap.add_argument("--nodes-per-gpu", type=int, default=1000,
                     help="multi-GPU weak scaling: nodes per rank (nodes x GPUs a multiple of 100; 1250 at "
                          "--gpus 8 gives BASELINE configs[4], 10000 nodes)")
+    ap.add_argument("--shard", default="stripes", choices=["stripes", "nodes"],
+                    help="multi-GPU partition: parameter-column stripes of every node (no exchange) "
+                         "or node shards with an RCCL halo exchange")
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
     return ap.parse_args()
@@ -372,6 +378,24 @@ def main():
             xa = xa[:, :p]
             xb = alloc()[:, :p]
         halo = 0
+        cols_local = p
+    elif args.shard == "stripes":
+        from niidmix.shard import StripedMixer
+        p = args.p or (1 << 20)
+        mixer = StripedMixer.dcliques(n_per_rank=args.nodes_per_gpu, clique_size=100, world=world,
+                                      rank=rank, interclique=args.interclique, device=dev, p=p,
+                                      mode="exact" if args.kernel.endswith("exact") else "fast")
+        n_local, n_total = mixer.n_local, mixer.n_total
+        cols_local, halo = mixer.p_local, 0
+        desc = (f"d-cliques N={n_total} ({n_total // 100} cliques x 100, {args.interclique} "
+                f"interclique, MH), P={p} split in {world} column stripes")
+        parallelism = (f"{world} parameter-column stripes of all {n_total} nodes (columns "
+                       f"[{mixer.c0}, {mixer.c1}) on rank {rank}); no data-path collective")
+        csr = None
+        gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
+        xa = mixer.empty()
+        xa.normal_(generator=gen)
+        xb = mixer.empty()
     else:
         from niidmix.shard import ShardedMixer
         p = args.p or (1 << 20)
@@ -380,6 +404,7 @@ def main():
                                       windows=args.windows)
         n_local, n_total = mixer.n_local, mixer.n_total
         halo = mixer.halo_rows
+        cols_local = p
         desc = (f"d-cliques N={n_total} ({n_total // 100} cliques x 100, {args.interclique} "
                 f"interclique, MH), {args.nodes_per_gpu} nodes per GPU; halo rows over RCCL")
         parallelism = (f"{world} clique-aligned node shards, RCCL (xGMI) halo exchange pipelined "
@@ -415,7 +440,7 @@ def main():
         step(xa, xb)
         xa, xb = xb, xa
     use_graph = world == 1 and (args.graph == "on" or
-                                (args.graph == "auto" and n_local * p * 4 < (256 << 20)))
+                                (args.graph == "auto" and n_local * cols_local * 4 < (256 << 20)))
     graph = None
     if use_graph:
         # the K timed rounds as ONE hipGraph (ping-pong unrolled); replayed once in the timed region
@@ -456,17 +481,17 @@ def main():
         region_s, launch_ms = tt.tolist()
     step_s = region_s / args.steps
     value = n_total * p * 4 / step_s / 1e9
-    copy_gbs = stream_copy_probe(n_local * p, dev)
+    copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
     if rank == 0:
         if kernel == "dense":
-            flops = 2.0 * n_local * n_local * p
+            flops = 2.0 * n_local * n_local * cols_local
             achieved = flops / (launch_ms / 1e3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                     "traffic": load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}")}
         else:
-            alg = 2.0 * n_local * p * 4
+            alg = 2.0 * n_local * cols_local * 4
             achieved = alg / (launch_ms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -494,10 +519,14 @@ def main():
                        "mode": mode, "parallelism": parallelism,
                        "launch_ms": round(launch_ms, 4), "halo_rows_rank0": halo,
                        "hipgraph": graph is not None,
-                       "slab_memory": ("hipMalloc" if args.hipmalloc_slabs or world > 1
+                       "slab_memory": ("hipMalloc" if args.hipmalloc_slabs or
+                                       (world > 1 and args.shard == "nodes")
                                        else "VMM 2 MiB chunks (niidmix_hbm_alloc)"),
                        "slab_layout": (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, "
-                                       f"{xa.shape[2]}]" if blocked else "row-major [N, P]"),
+                                       f"{xa.shape[2]}]" if xa.dim() == 3 and
+                                       (blocked or args.shard == "stripes") else
+                                       "window-blocked [K, rows_in, w]" if xa.dim() == 3 else
+                                       "row-major [N, P]"),
                        "stream_copy_GBs": round(copy_gbs, 1),
                        "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
                                                if roof["unit"] == "GB/s" else None)},

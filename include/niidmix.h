@@ -101,7 +101,10 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  * verifies that it reproduces every W entry; see DESIGN.md.  All arrays are device pointers.
  *   clique_ptr   [n_cliques+1] int32 offsets into the member arrays
  *   member_row   [n_members] int32 row index (input row == output row)
- *   member_group [n_members] int32 group id in [0, n_groups)
+ *   member_group [n_members] int32 group id in [0, n_groups), optionally OR-ed with
+ *                NIIDMIX_MEMBER_GATEWAY when the member's row is also some residual entry's source
+ *                (res_col): a load-policy hint only (that row is loaded temporally so the gather
+ *                hits L2), never changes results
  *   coef         [n_members * (1 + n_groups)] fp32: a_m, then c_{m,0..n_groups-1}
  *   res_ptr      [n_members+1] int32 offsets into res_col/res_val (residual sparse terms)
  *   res_col      [n_res] int32 input rows, res_val [n_res] fp32
@@ -114,6 +117,8 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *                kernel whose second read is served from L2 / Infinity Cache
  *   max_clique_res  largest number of residual terms of one clique (informational, >= 0)
  *   n_groups     1..4 */
+#define NIIDMIX_MEMBER_GATEWAY 256
+
 typedef struct niidmix_clique_plan {
     int32_t n_cliques;
     int32_t n_members;

@@ -229,6 +229,8 @@ __device__ __forceinline__ void clique_item(int64_t t, int32_t n_cliques, int64_
     chunk = (skew && base < nc) ? (base + (int64_t)cq * skew) % nc : base;
 }
 
+constexpr int kMemberGroupMask = NIIDMIX_MEMBER_GATEWAY - 1;   // member_group: id | hint bits
+
 template <int G, int RW>
 struct CliqueDesc {        // one work item's descriptors, lane-parallel
     int32_t m0, M;         // wave-uniform: first member, members (0 past p)
@@ -338,8 +340,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         for (int e = 0; e < V; ++e) v[r][e] = 0.f;
         if (wave + WAVES * r < M) {
             const int64_t row = __builtin_amdgcn_readlane(d.row, r);
+            // a gateway row (NIIDMIX_MEMBER_GATEWAY) is gathered again as another clique's
+            // residual term: a temporal load keeps it in L2 for that gather (wave-uniform branch)
+            const bool gw = (__builtin_amdgcn_readlane(d.grp, r) & NIIDMIX_MEMBER_GATEWAY) != 0;
             if (act) {
-                if (NTL) ldv_nt<V>(xc + row * ld_x + lo, v[r]);
+                if (NTL && !gw) ldv_nt<V>(xc + row * ld_x + lo, v[r]);
                 else ldv<V>(xc + row * ld_x + lo, v[r]);
             }
         }
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
             if (wave + WAVES * r < M) {
-                const int gr = __builtin_amdgcn_readlane(d.grp, r);
+                const int gr = __builtin_amdgcn_readlane(d.grp, r) & kMemberGroupMask;
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     if (gr == g) {
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (k + u < ke) {
-                    const int gr = member_group[k + u];
+                    const int gr = member_group[k + u] & kMemberGroupMask;
 #pragma unroll
                     for (int g = 0; g < G; ++g) s[g] += gr == g ? v[u] : 0.f;
                 }

@@ -31,6 +31,7 @@ EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
 AVERAGE_ONLY = 2
 LOW_DEGREE = 4
 MEAN = 8
+MEMBER_GATEWAY = 256        # member_group hint bit (include/niidmix.h NIIDMIX_MEMBER_GATEWAY)
 
 
 def _stream(t):
@@ -352,7 +353,11 @@ class Mixer:
             p = self.plan
             self.p_clique_ptr = torch.from_numpy(p.clique_ptr).to(dev)
             self.p_member_row = torch.from_numpy(p.member_row).to(dev)
-            self.p_member_group = torch.from_numpy(p.member_group).to(dev)
+            grp = p.member_group.copy()
+            if os.environ.get("NIIDMIX_GATEWAY_HINT", "1") != "0" and len(p.res_col):
+                # rows gathered as residual terms: loaded temporally by their own clique's item
+                grp[np.isin(p.member_row, p.res_col)] |= MEMBER_GATEWAY
+            self.p_member_group = torch.from_numpy(grp).to(dev)
             self.p_coef = torch.from_numpy(np.ascontiguousarray(p.coef)).to(dev)
             self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
             self.p_res_col = torch.from_numpy(p.res_col).to(dev)

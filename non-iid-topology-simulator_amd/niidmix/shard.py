@@ -1,4 +1,13 @@
-"""Multi-GPU mixing: simulated nodes sharded across GPUs, cross-shard edges carried by RCCL.
+"""Multi-GPU mixing: two partitions of one round across GPUs (one process per GPU).
+
+COLUMN STRIPES (StripedMixer, the default of bench.py --gpus N): the round is independent per
+parameter column (Θ'[:, c] = Wᵀ Θ[:, c], d_sgd.py:96-116 mixes every tensor element-wise), so rank
+r owns parameter columns [c0, c1) of EVERY node and mixes them with no exchange at all.  Results
+are the single-GPU bits of those columns.  This is the natural split of the simulator, which
+holds all nodes' models in one process.
+
+NODE SHARDS (ShardedMixer): simulated nodes sharded across GPUs, cross-shard edges carried by
+RCCL, for callers whose nodes' full parameter vectors must live on their own rank.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  The path shards
 naturally: every output row depends only on the pre-round rows of its in-neighbours, so one
@@ -322,6 +331,69 @@ class ShardedMixer:
                 self.transport.wait(pending[k])
             cw = min(self.w, self.p - k * self.w)
             self.compute(x[k][:, :cw], out[k][:self.n_local, :cw], kernel=kernel, mode=mode)
+        if events is not None:
+            events[1].record(cur)
+        return out
+
+
+def column_stripe(p, world, rank, align=1024):
+    """Rank r's parameter columns [c0, c1): ceil(p / align) column units of `align` dealt as evenly
+    as possible in rank order (stripes stay block-aligned for the column-blocked layout)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} not in world of {world}")
+    units = -(-p // align)
+    base, extra = divmod(units, world)
+    u0 = rank * base + min(rank, extra)
+    u1 = u0 + base + (1 if rank < extra else 0)
+    return min(u0 * align, p), min(u1 * align, p)
+
+
+class StripedMixer:
+    """One rank's column stripe of the round: every node, columns [c0, c1), no exchange.
+
+    Fast mode keeps the stripe device-resident in the column-blocked layout (niidmix.memory) and
+    runs the clique kernel; exact mode (or a topology without a clique plan) uses a row-major
+    [N, c1 - c0] slab and the Mixer's kernel choice.  Either way the stripe's result is bitwise the
+    single-GPU result's columns [c0, c1) (same kernel, same per-column arithmetic)."""
+
+    def __init__(self, csr, cliques, world, rank, device, p, mode="fast", align=1024):
+        from . import ops
+        self.world, self.rank, self.p = world, rank, p
+        self.device = torch.device(device)
+        self.c0, self.c1 = column_stripe(p, world, rank, align)
+        self.p_local = self.c1 - self.c0
+        self.n_total = self.n_local = csr.n
+        self.halo_rows = 0
+        self.mode = mode
+        self.mixer = ops.Mixer(csr=csr, cliques=cliques, device=self.device)
+        self.blocked = (mode == "fast" and self.mixer.plan is not None and
+                        self.mixer.plan.max_clique <= 256 and self.p_local % 4 == 0)
+
+    @classmethod
+    def dcliques(cls, n_per_rank, clique_size, world, rank, interclique, device, p, seed=1337,
+                 mode="fast"):
+        from .generate import dcliques_csr
+        csr, cliques = dcliques_csr(n_per_rank * world, clique_size, interclique, seed)
+        return cls(csr, cliques, world, rank, device, p, mode=mode)
+
+    def empty(self):
+        from . import memory
+        if self.blocked:
+            return memory.empty_blocked(self.n_total, self.p_local, self.device)
+        return memory.empty_slab(self.n_total, self.p_local, self.device)
+
+    def kernel_for(self, mode="fast", x=None):
+        return "clique" if self.blocked and mode == "fast" else self.mixer.kernel_for(mode)
+
+    def __call__(self, x, out, kernel=None, mode=None, events=None):
+        mode = mode or self.mode
+        cur = torch.cuda.current_stream(self.device)
+        if events is not None:
+            events[0].record(cur)
+        if self.blocked and mode == "fast":
+            self.mixer.mix_blocked(x, out, self.p_local)
+        else:
+            self.mixer(x, out=out, kernel=kernel, mode=mode)
         if events is not None:
             events[1].record(cur)
         return out

@@ -102,3 +102,42 @@ def test_sharded_rounds_loopback(world, inter, gpu, oracle_mod):
             assert oracle_mod.bitwise_equal(got, ref)
         else:
             assert np.max(np.abs(got - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_striped_mixer_equals_single_gpu(world, gpu, oracle_mod):
+    """Every rank's column stripe (blocked slab, clique kernel) is bitwise the single-GPU blocked
+    round's columns; exact-mode stripes are bitwise the oracle."""
+    from niidmix import memory
+    from niidmix.generate import dcliques_csr
+    from niidmix.ops import Mixer
+    from niidmix.shard import StripedMixer
+    csr, cliques = dcliques_csr(1000 * world // 2, 100, "fully-connected", 1337)
+    p = world * 1024 + 512 if world == 2 else 7 * 1024 + 256
+    x = torch.randn(csr.n, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(world))
+    full = Mixer(csr=csr, cliques=cliques, device=gpu)
+    yb = memory.empty_blocked(csr.n, p, gpu)
+    full.mix_blocked(memory.to_blocked(x), yb, p)
+    y_full = memory.from_blocked(yb, p)
+    covered = 0
+    for r in range(world):
+        sm = StripedMixer(csr, cliques, world, r, gpu, p)
+        if sm.p_local == 0:
+            continue
+        assert sm.blocked
+        xs = memory.to_blocked(x[:, sm.c0:sm.c1].contiguous())
+        ys = sm.empty()
+        sm(xs, ys)
+        assert torch.equal(memory.from_blocked(ys, sm.p_local), y_full[:, sm.c0:sm.c1]), r
+        covered += sm.p_local
+        if r == 0:
+            se = StripedMixer(csr, cliques, world, r, gpu, p, mode="exact")
+            assert not se.blocked
+            xe = se.empty()
+            xe.copy_(x[:, se.c0:se.c1])
+            ye = se.empty()
+            se(xe, ye)
+            ref = oracle_mod.mix_exact_c(x[:, se.c0:se.c1].cpu().numpy(), csr.row_ptr, csr.col,
+                                         csr.val)
+            assert oracle_mod.bitwise_equal(ye.cpu().numpy(), ref)
+    assert covered == p

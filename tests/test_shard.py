@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import load_golden
-from niidmix.shard import ShardPlan, ShardedMixer, window_layout
+from niidmix.shard import ShardPlan, ShardedMixer, column_stripe, window_layout
 from niidmix.topology import MixCSR
 
 
@@ -115,3 +115,62 @@ def test_gloo_sharded_rounds(world, name, oracle_mod):
     for rank, nodes, res in got:
         full[nodes] = res
     assert oracle_mod.bitwise_equal(full, ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("p", [1, 1000, 1024, 4096 + 4, 1 << 20, 3 * 1024 + 512])
+def test_column_stripes_partition(world, p):
+    """Stripes tile [0, p) in rank order, start on block boundaries and are balanced to a block."""
+    stripes = [column_stripe(p, world, r) for r in range(world)]
+    assert stripes[0][0] == 0 and stripes[-1][1] == p
+    for (a0, a1), (b0, b1) in zip(stripes, stripes[1:]):
+        assert a1 == b0
+    assert all((c0 % 1024 == 0 or c0 == p) and c0 <= c1 for c0, c1 in stripes)
+    widths = [c1 - c0 for c0, c1 in stripes]
+    assert max(widths) <= -(-p // world) + 1024        # block-granular balance
+    with pytest.raises(ValueError):
+        column_stripe(p, world, world)
+
+
+def _stripe_worker(rank, world, port, name, p, rounds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        g = load_golden(name)
+        c0, c1 = column_stripe(p, world, rank, align=16)
+        x = np.ascontiguousarray(g["x"][:, c0:c1])
+        for _ in range(rounds):             # no exchange: each stripe's rounds are independent
+            x = oracle.mix_exact_c(x, g["row_ptr"], g["col"], g["val"])
+        parts = [None] * world
+        dist.all_gather_object(parts, (c0, c1, x))
+        if rank == 0:
+            q.put(parts)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name", [(2, "dcliques1000_fc_p64"), (3, "ring100_p257")])
+def test_gloo_striped_rounds(world, name, oracle_mod):
+    """Column stripes over gloo: the gathered stripes of R rounds equal the single-process rounds
+    bit for bit (the round is independent per parameter column)."""
+    g = load_golden(name)
+    p = g["x"].shape[1]
+    rounds = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stripe_worker, args=(r, world, port, name, p, rounds, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    parts = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref = g["x"].copy()
+    for _ in range(rounds):
+        ref = oracle_mod.mix_exact_c(ref, g["row_ptr"], g["col"], g["val"])
+    got = np.concatenate([x for _, _, x in parts], axis=1)
+    assert [c for c0, c1, _ in parts for c in (c0, c1)][0] == 0 and parts[-1][1] == p
+    assert oracle_mod.bitwise_equal(got, ref)
