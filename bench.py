@@ -330,12 +330,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # NIIDMIX_BENCH_BACKEND=gloo: rehearse the N-rank path with every rank on the visible GPU(s)
+    # (one-GPU box; timing not meaningful).  The driver's runs use RCCL, one GPU per rank.
+    backend = os.environ.get("NIIDMIX_BENCH_BACKEND", "nccl")
+    gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from niidmix import memory, ops
     if args.workload != "mix" and world > 1:
@@ -476,7 +483,8 @@ def main():
     else:
         launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist:
-        tt = torch.tensor([region_s, launch_ms], device=dev, dtype=torch.float64)
+        tt = torch.tensor([region_s, launch_ms], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         region_s, launch_ms = tt.tolist()
     step_s = region_s / args.steps
@@ -484,18 +492,20 @@ def main():
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
     if rank == 0:
+        # PMC traffic is profiled per single-GPU config (profiles/traffic.json)
+        traffic = load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}") if world == 1 else None
         if kernel == "dense":
             flops = 2.0 * n_local * n_local * cols_local
             achieved = flops / (launch_ms / 1e3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                    "traffic": load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}")}
+                    "traffic": traffic}
         else:
             alg = 2.0 * n_local * cols_local * 4
             achieved = alg / (launch_ms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}")}
+                    "traffic": traffic}
         e2e = None
         if world == 1 and args.e2e and args.workload == "grad-clique":
             del xa, xb
