@@ -311,6 +311,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     constexpr bool NO_RES = (FL & 4) != 0, NO_RED = (FL & 8) != 0;
     constexpr bool PLAIN_ST = (FL & 16) != 0;   // write-back (L2) stores instead of non-temporal
     constexpr int RQ = 2;                     // residual rows per wave held in registers
+    // overflow residual gathers in flight per batch (N=8 stripes: 1.494 ms vs 1.506 ms one at a
+    // time); G >= 3 tiles are at the register limit already
+    constexpr int OVB = G <= 2 ? 3 : 1;
     constexpr int64_t CW = 64 * V;            // columns per work item
     __shared__ float red[G][WAVES][kWave * V];
     __shared__ float tot[G][kWave * V];
@@ -415,21 +418,31 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     }
     // overflow: entries past the RQ held per wave, and clique entries past the RW fetched
     // lane-parallel (scalar loads, one gather at a time)
-    for (; mine; mine &= mine - 1) {
-        const int j = __builtin_ctzll(mine);
-        const int64_t row = __builtin_amdgcn_readlane(d.rsrc, j);
-        float xo[V];
+    // (OVB gathers in flight per batch; the registers of xr[] are free again here)
+    while (mine) {
+        float xo[OVB][V];
+        int jo[OVB];
 #pragma unroll
-        for (int e = 0; e < V; ++e) xo[e] = 0.f;
-        if (act) ldv<V>(xc + row * ld_x + lo, xo);
-        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), j));
-        const int slot = __builtin_amdgcn_readlane(d.rk, j) / WAVES;
+        for (int b = 0; b < OVB; ++b) {
+            jo[b] = mine ? __builtin_ctzll(mine) : -1;
+            mine &= mine - 1;
+            const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jo[b] >= 0 ? jo[b] : 0);
 #pragma unroll
-        for (int r = 0; r < RPW; ++r)
-            if (slot == r) {
+            for (int e = 0; e < V; ++e) xo[b][e] = 0.f;
+            if (act && jo[b] >= 0) ldv<V>(xc + row * ld_x + lo, xo[b]);
+        }
 #pragma unroll
-                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[e], v[r][e]);
-            }
+        for (int b = 0; b < OVB; ++b) {
+            if (jo[b] < 0) break;                                       // wave-uniform
+            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), jo[b]));
+            const int slot = __builtin_amdgcn_readlane(d.rk, jo[b]) / WAVES;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r)
+                if (slot == r) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[b][e], v[r][e]);
+                }
+        }
     }
     for (int32_t q = d.cr0 + nl; q < d.cr0 + ncr; ++q) {
         const int k = res_member[q];
