@@ -702,6 +702,109 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
 }
 
 // ----------------------------------------------------------------------------------------------
+// One-pass big-clique mixing, register-resident (257..32*R members).  Work item = (clique, 32
+// columns = 128 B of every member row); a block of 16 waves holds the whole item in VGPRs: lane =
+// (half h, column lc), wave w holds members 2*(w*R + i) + h, i < R.  All R row loads of a lane
+// issue back to back, the per-group column sums are reduced over the half-waves (swizzle) and the
+// 16 waves (LDS), and the outputs y = a x + sum_g c_g S_g (+ residual terms) are computed from the
+// registers -- each member row is read from HBM ONCE (the two-pass kernel reads it twice).  The
+// clique's metadata (rows, coefficients, residual ranges) is staged in LDS and re-staged only when
+// a block's clique changes: items are clique-major, so a grid-stride block stays on one clique.
+constexpr int kBigRegWaves = 16;
+constexpr int kBigRegCols = 32;
+template <int G, int R, int OCC>
+__global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_mix_bigclique_reg(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
+    const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
+    const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8) {
+    constexpr int MMAX = kBigRegWaves * 2 * R;
+    __shared__ int32_t s_row[MMAX];
+    __shared__ int32_t s_grp[MMAX];
+    __shared__ int32_t s_res[MMAX + 1];
+    __shared__ float s_cf[MMAX * (1 + G)];
+    __shared__ float red[G][kBigRegWaves][kBigRegCols];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int h = lane >> 5, lc = lane & (kBigRegCols - 1);
+    const int64_t n_items = (int64_t)n_cliques * nch8 * 8;
+    int32_t cur = -1, m0 = 0, M = 0;
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int32_t cq = (int32_t)(local / nch8);
+        const int64_t chunk = (local % nch8) * 8 + xcd;
+        const int64_t c0 = chunk * kBigRegCols;
+        if (c0 >= p) continue;                               // block-uniform
+        if (cq != cur) {                                     // block-uniform
+            __syncthreads();                                 // previous item done with s_*
+            cur = cq;
+            m0 = clique_ptr[cq];
+            M = clique_ptr[cq + 1] - m0;
+            for (int k = threadIdx.x; k < M; k += blockDim.x) {
+                s_row[k] = member_row[m0 + k];
+                s_grp[k] = member_group[m0 + k] & kMemberGroupMask;
+#pragma unroll
+                for (int g = 0; g <= G; ++g) s_cf[k * (1 + G) + g] = coef[(int64_t)(m0 + k) * (1 + G) + g];
+            }
+            for (int k = threadIdx.x; k <= M; k += blockDim.x) s_res[k] = res_ptr[m0 + k];
+            __syncthreads();
+        }
+        const bool act = c0 + lc < p;
+        const unsigned lo = act ? (unsigned)lc : 0u;
+        const float *xc = x + c0 + lo;
+        float v[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int k = 2 * (wave * R + i) + h;
+            v[i] = k < M ? __builtin_nontemporal_load(xc + (int64_t)s_row[k] * ld_x) : 0.f;
+        }
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            if (G == 1) {
+                s[0] += v[i];                                // rows past M hold 0
+            } else {
+                const int k = 2 * (wave * R + i) + h;
+                const int gr = k < M ? s_grp[k] : -1;
+#pragma unroll
+                for (int g = 0; g < G; ++g) s[g] += gr == g ? v[i] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            s[g] += __shfl_xor(s[g], 32);
+            if (h == 0) red[g][wave][lc] = s[g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < kBigRegWaves; ++w) a += red[g][w][lc];
+            s[g] = a;
+        }
+        __syncthreads();                                      // red[] is rewritten by the next item
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int k = 2 * (wave * R + i) + h;
+            if (k < M) {
+                const float *cf = s_cf + k * (1 + G);
+                float o = cf[0] * v[i];
+#pragma unroll
+                for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g], o);
+                for (int32_t q = s_res[k]; q < s_res[k + 1]; ++q)
+                    o = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x], o);
+                if (act) __builtin_nontemporal_store(o, y + (int64_t)s_row[k] * ld_y + c0 + lc);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Block-staged CSR mixing (exact or fast).  Output rows are grouped into blocks (the cliques); a
 // block's distinct source rows (members + remote neighbours, <= 256) are staged ONCE per column
 // chunk in LDS, then every output row accumulates its CSR entries in the reference's order from
@@ -1557,15 +1660,44 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         // 8 waves x 16 blocks/CU 2.36 ms; capping residency (to keep the pass-2 re-read in the
         // Infinity Cache) was slower: 8x4 2.57, 16x1 2.95 ms.  NIIDMIX_BIG=<waves>x<blocks per CU>
         // overrides (tuning).
-        int waves = 8, bpc = 16;
-        if (const char *e = getenv("NIIDMIX_BIG")) sscanf(e, "%dx%d", &waves, &bpc);
-        if (bpc < 1) bpc = 1;
         static int n_cu = 0;
         if (!n_cu) {
             int dev = 0;
             (void)hipGetDevice(&dev);
             if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
         }
+        const char *big_env = getenv("NIIDMIX_BIG");         // "WxB": the two-pass kernel (tuning)
+        if (big_env && !strcmp(big_env, "reg")) big_env = nullptr;
+        if (!big_env && plan->max_clique <= 2 * kBigRegWaves * 32) {
+            // one pass, the item register-resident (k_mix_bigclique_reg): 2 blocks of 16 waves per
+            // CU (<= 64 VGPRs), or 1 block where a 64-VGPR budget would spill (R = 32 with groups)
+            const int64_t nch8 = ((p + kBigRegCols - 1) / kBigRegCols + 7) / 8;
+            const int64_t items = (int64_t)plan->n_cliques * nch8 * 8;
+            const bool r16 = plan->max_clique <= 2 * kBigRegWaves * 16;
+            const int bpc = (r16 || plan->n_groups == 1) ? 2 : 1;
+            int64_t gsz = (int64_t)bpc * n_cu;
+            if (gsz > items) gsz = items;
+            const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
+#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8)
+            if (r16) {
+                switch (plan->n_groups) {
+                case 1: NIIDMIX_BIGREG(1, 16, 8); break; case 2: NIIDMIX_BIGREG(2, 16, 8); break;
+                case 3: NIIDMIX_BIGREG(3, 16, 8); break; case 4: NIIDMIX_BIGREG(4, 16, 8); break;
+                default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+                }
+            } else {
+                switch (plan->n_groups) {
+                case 1: NIIDMIX_BIGREG(1, 32, 8); break; case 2: NIIDMIX_BIGREG(2, 32, 4); break;
+                case 3: NIIDMIX_BIGREG(3, 32, 4); break; case 4: NIIDMIX_BIGREG(4, 32, 4); break;
+                default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+                }
+            }
+#undef NIIDMIX_BIGREG
+            return check_launch("k_mix_bigclique_reg");
+        }
+        int waves = 8, bpc = 16;
+        if (big_env) sscanf(big_env, "%dx%d", &waves, &bpc);
+        if (bpc < 1) bpc = 1;
         const int64_t n_ch = (p + kWave - 1) / kWave;
         const int64_t items = (int64_t)plan->n_cliques * ((n_ch + 7) / 8) * 8;
         int64_t gsz = ((int64_t)bpc * n_cu + 7) / 8 * 8;

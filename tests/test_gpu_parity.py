@@ -343,3 +343,31 @@ def test_clique_many_gateways(n, gpu, oracle_mod):
     yb = memory.empty_blocked(n, 256, gpu)
     m.mix_blocked(memory.to_blocked(x), yb, 256)
     assert np.array_equal(memory.from_blocked(yb, 256).cpu().numpy(), y)
+
+
+@pytest.mark.parametrize("n,size,inter,p", [(1200, 600, "ring", 4096 + 20), (900, 300, "fully-connected", 999),
+                                            (1000, 1000, "ring", 33), (2000, 500, "smallworld", 250)])
+def test_bigclique_one_pass(n, size, inter, p, gpu, oracle_mod, monkeypatch):
+    """Big cliques (> 256 members): the one-pass register-resident kernel (k_mix_bigclique_reg,
+    R = 16 and 32, one or more degree groups, gateway residual terms, ragged column tails) within
+    the tolerance of the oracle, and equal to the two-pass kernel (NIIDMIX_BIG=8x16) up to the
+    summation order."""
+    from niidmix import ops
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(n, size, inter, 1337)
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.plan is not None and m.plan.max_clique > 256, m.plan_reason
+    gen = torch.Generator().manual_seed(p)
+    xh = torch.randn(n, p, generator=gen)
+    x = xh.to(gpu)
+    monkeypatch.delenv("NIIDMIX_BIG", raising=False)
+    y = m(x, kernel="clique").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+    assert ok, worst
+    monkeypatch.setenv("NIIDMIX_BIG", "8x16")
+    y2 = m(x, kernel="clique").cpu().numpy()
+    ok, worst = oracle_mod.check_tolerance(y2, ref, bound, rtol=RTOL)
+    assert ok, worst
+    assert np.max(np.abs(y - y2)) <= 1e-5 * np.max(bound)
