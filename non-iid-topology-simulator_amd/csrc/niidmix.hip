@@ -1589,9 +1589,11 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
     const int vw = (p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && (align & 15) == 0) ? 4
                  : (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
-    // NIIDMIX_CSR_SPL=4: 4x wider work items (tuning; measured slower on ring-100, P=62006)
+    // work-item width: 2 chunks per wave for a low-degree graph (ring-100, P = 62006: 15.7 us vs
+    // 16.6 us for 1 chunk and 16.6 us for 4 chunks, whose 142 VGPRs cap occupancy at 3 waves/SIMD;
+    // profiles/r01/ring100_spl.txt), else 1.  NIIDMIX_CSR_SPL=1|2|4 overrides (tuning).
     const char *spl_env = getenv("NIIDMIX_CSR_SPL");
-    const int spl = (spl_env && atoi(spl_env) == 4) ? 4 : 1;
+    const int spl = spl_env ? (atoi(spl_env) == 4 ? 4 : atoi(spl_env) == 2 ? 2 : 1) : (low_degree ? 2 : 1);
     const int64_t n_chunks = (p + kChunk * spl - 1) / (kChunk * spl);
     const int64_t n_row_groups = (n_rows + 3) / 4;
     const int64_t n_items = n_row_groups * ((n_chunks + 7) / 8) * 8;
@@ -1600,7 +1602,7 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     const bool lowdeg = low_degree != 0;
 #define NIIDMIX_CSR(E, V, S, UU) hipLaunchKernelGGL((k_mix_csr<E, V, S, UU>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, row_ptr, col, val, n_row_groups, n_items, kflags)
 #define NIIDMIX_CSR_U(E, V, S) do { if (lowdeg) NIIDMIX_CSR(E, V, S, 4); else NIIDMIX_CSR(E, V, S, 8); } while (0)
-#define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR_U(E, V, 4); else NIIDMIX_CSR_U(E, V, 1); } while (0)
+#define NIIDMIX_CSR_S(E, V) do { if (spl == 4) NIIDMIX_CSR_U(E, V, 4); else if (spl == 2) NIIDMIX_CSR_U(E, V, 2); else NIIDMIX_CSR_U(E, V, 1); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) {
         if (vw == 4) NIIDMIX_CSR_S(true, 4); else if (vw == 2) NIIDMIX_CSR_S(true, 2); else NIIDMIX_CSR_S(true, 1);
     } else {
