@@ -788,18 +788,30 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
             s[g] = a;
         }
         __syncthreads();                                      // red[] is rewritten by the next item
+        // outputs in place, residual (gateway) gathers all before the first store: a load between
+        // two stores would make its wait drain the earlier stores (vmcnt counts stores on CDNA)
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int k = 2 * (wave * R + i) + h;
-            if (k < M) {
-                const float *cf = s_cf + k * (1 + G);
-                float o = cf[0] * v[i];
+            const float *cf = s_cf + (k < M ? k : 0) * (1 + G);
+            float o = cf[0] * v[i];
 #pragma unroll
-                for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g], o);
-                for (int32_t q = s_res[k]; q < s_res[k + 1]; ++q)
-                    o = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x], o);
-                if (act) __builtin_nontemporal_store(o, y + (int64_t)s_row[k] * ld_y + c0 + lc);
+            for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g], o);
+            v[i] = o;
+        }
+        if (s_res[M] > s_res[0]) {                            // block-uniform: any gateway edges
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const int k = 2 * (wave * R + i) + h;
+                if (k < M)
+                    for (int32_t q = s_res[k]; q < s_res[k + 1]; ++q)
+                        v[i] = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x], v[i]);
             }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int k = 2 * (wave * R + i) + h;
+            if (k < M && act) __builtin_nontemporal_store(v[i], y + (int64_t)s_row[k] * ld_y + c0 + lc);
         }
     }
 }
