@@ -373,7 +373,7 @@ def main():
         if k0 == "auto":
             k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
         if (args.layout == "blocked" and not args.hipmalloc_slabs and p % 4 == 0 and
-                ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 256) or
+                ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 1024) or
                  args.workload == "grad-clique")):
             # device-resident node state in the column-blocked layout [K, N, 1024]
             xa = memory.empty_blocked(n_local, p, dev)

@@ -113,8 +113,9 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *                with the member descriptors, so the gateway-row gathers issue right behind the
  *                member-row loads)
  *   max_clique   largest clique size: <= 256 selects a register tile (one HBM read per
- *                parameter); larger cliques (e.g. fully-connected = one clique) use a two-pass
- *                kernel whose second read is served from L2 / Infinity Cache
+ *                parameter); 257..1024 (e.g. fully-connected = one clique) the one-pass
+ *                big-clique kernel (a 32-column item of every member held in registers, one HBM
+ *                read per parameter); larger cliques a two-pass kernel (rows read twice)
  *   max_clique_res  largest number of residual terms of one clique (informational, >= 0)
  *   n_groups     1..4 */
 #define NIIDMIX_MEMBER_GATEWAY 256
@@ -168,7 +169,8 @@ int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  *   base + (c / block_cols) * block_stride + r * ld + c % block_cols.
  * block_cols: a power of two >= 256.  This is the layout niidmix keeps device-resident node state
  * in (block_cols = 1024): a clique's member rows then sit 4 KiB apart instead of P*4 bytes, which
- * measured robust to the slab's physical placement.  Cliques of <= 256 members. */
+ * measured robust to the slab's physical placement.  Cliques of <= 256 members use
+ * the register tile, 257..1024 members the one-pass big-clique kernel (32-column items). */
 int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
                                    int64_t block_cols, int64_t block_stride_x,
                                    int64_t block_stride_y, const niidmix_clique_plan *plan,

@@ -718,7 +718,10 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
-    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8) {
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8,
+    int bc_shift, int64_t bs_x, int64_t bs_y) {
+    // column c of row r: x[(c >> bc_shift) * bs_x + r * ld_x + (c & (2^bc_shift - 1))] -- the
+    // column-blocked layout [P / B, N, B] (ld = B), or row-major with bc_shift = 62, bs = 0
     constexpr int MMAX = kBigRegWaves * 2 * R;
     __shared__ int32_t s_row[MMAX];
     __shared__ int32_t s_grp[MMAX];
@@ -753,7 +756,9 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
         }
         const bool act = c0 + lc < p;
         const unsigned lo = act ? (unsigned)lc : 0u;
-        const float *xc = x + c0 + lo;
+        const int64_t cin = c0 & (((int64_t)1 << bc_shift) - 1);
+        const float *xc = x + (c0 >> bc_shift) * bs_x + cin + lo;
+        float *yc = y + (c0 >> bc_shift) * bs_y + cin + lc;
         float v[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
@@ -811,7 +816,7 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int k = 2 * (wave * R + i) + h;
-            if (k < M && act) __builtin_nontemporal_store(v[i], y + (int64_t)s_row[k] * ld_y + c0 + lc);
+            if (k < M && act) __builtin_nontemporal_store(v[i], yc + (int64_t)s_row[k] * ld_y);
         }
     }
 }
@@ -1626,6 +1631,47 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     return check_launch("k_mix_csr");
 }
 
+static int cu_count() {
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
+    }
+    return n_cu;
+}
+
+// One-pass big-clique launch (k_mix_bigclique_reg) for cliques of 257..1024 members: 2 blocks of
+// 16 waves per CU (<= 64 VGPRs), or 1 block where a 64-VGPR budget would spill (R = 32 with
+// groups).  Row-major slabs: bc_shift 62, block strides 0; column-blocked slabs: B = 2^bc_shift.
+static int launch_bigclique_reg(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                                const niidmix_clique_plan *plan, int bc_shift, int64_t bs_x,
+                                int64_t bs_y, hipStream_t s) {
+    const int64_t nch8 = ((p + kBigRegCols - 1) / kBigRegCols + 7) / 8;
+    const int64_t items = (int64_t)plan->n_cliques * nch8 * 8;
+    const bool r16 = plan->max_clique <= 2 * kBigRegWaves * 16;
+    const int bpc = (r16 || plan->n_groups == 1) ? 2 : 1;
+    int64_t gsz = (int64_t)bpc * cu_count();
+    if (gsz > items) gsz = items;
+    const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
+#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y)
+    if (r16) {
+        switch (plan->n_groups) {
+        case 1: NIIDMIX_BIGREG(1, 16, 8); break; case 2: NIIDMIX_BIGREG(2, 16, 8); break;
+        case 3: NIIDMIX_BIGREG(3, 16, 8); break; case 4: NIIDMIX_BIGREG(4, 16, 8); break;
+        default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+        }
+    } else {
+        switch (plan->n_groups) {
+        case 1: NIIDMIX_BIGREG(1, 32, 8); break; case 2: NIIDMIX_BIGREG(2, 32, 4); break;
+        case 3: NIIDMIX_BIGREG(3, 32, 4); break; case 4: NIIDMIX_BIGREG(4, 32, 4); break;
+        default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+        }
+    }
+#undef NIIDMIX_BIGREG
+    return check_launch("k_mix_bigclique_reg");
+}
+
 int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
                                    int64_t block_cols, int64_t block_stride_x,
                                    int64_t block_stride_y, const niidmix_clique_plan *plan,
@@ -1643,10 +1689,14 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
     if (block_stride_x < ld || block_stride_y < ld)
         return set_error(NIIDMIX_EINVAL, "block stride < row stride");
     if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
-    if (plan->max_clique > 256) return set_error(NIIDMIX_EUNSUPPORTED, "blocked slabs: cliques of <= 256 members");
+    if (plan->max_clique > 2 * kBigRegWaves * 32)
+        return set_error(NIIDMIX_EUNSUPPORTED, "blocked slabs: cliques of <= 1024 members");
     if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
     const bool vec4 = (ld % 4 == 0) && (block_stride_x % 4 == 0) && (block_stride_y % 4 == 0) &&
                       aligned16(x) && aligned16(y);
+    if (plan->max_clique > 256)                               // one pass, 32-column items
+        return launch_bigclique_reg(x, ld, y, ld, p, plan, __builtin_ctzll((unsigned long long)block_cols),
+                                    block_stride_x, block_stride_y, reinterpret_cast<hipStream_t>(stream));
     BlockGeom bg;
     bg.cpb_shift = __builtin_ctzll((unsigned long long)(block_cols / 256));
     bg.bs_x = block_stride_x;
@@ -1654,6 +1704,8 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
     return launch_clique_tiled(x, ld, y, ld, p, plan, vec4, reinterpret_cast<hipStream_t>(stream), bg);
 }
 
+// One-pass big-clique launch (k_mix_bigclique_reg), row-major (bc_shift 62, block strides 0) or
+// column-blocked slabs.
 int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                            const niidmix_clique_plan *plan, void *stream) {
     if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
@@ -1682,33 +1734,8 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         }
         const char *big_env = getenv("NIIDMIX_BIG");         // "WxB": the two-pass kernel (tuning)
         if (big_env && !strcmp(big_env, "reg")) big_env = nullptr;
-        if (!big_env && plan->max_clique <= 2 * kBigRegWaves * 32) {
-            // one pass, the item register-resident (k_mix_bigclique_reg): 2 blocks of 16 waves per
-            // CU (<= 64 VGPRs), or 1 block where a 64-VGPR budget would spill (R = 32 with groups)
-            const int64_t nch8 = ((p + kBigRegCols - 1) / kBigRegCols + 7) / 8;
-            const int64_t items = (int64_t)plan->n_cliques * nch8 * 8;
-            const bool r16 = plan->max_clique <= 2 * kBigRegWaves * 16;
-            const int bpc = (r16 || plan->n_groups == 1) ? 2 : 1;
-            int64_t gsz = (int64_t)bpc * n_cu;
-            if (gsz > items) gsz = items;
-            const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
-#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8)
-            if (r16) {
-                switch (plan->n_groups) {
-                case 1: NIIDMIX_BIGREG(1, 16, 8); break; case 2: NIIDMIX_BIGREG(2, 16, 8); break;
-                case 3: NIIDMIX_BIGREG(3, 16, 8); break; case 4: NIIDMIX_BIGREG(4, 16, 8); break;
-                default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
-                }
-            } else {
-                switch (plan->n_groups) {
-                case 1: NIIDMIX_BIGREG(1, 32, 8); break; case 2: NIIDMIX_BIGREG(2, 32, 4); break;
-                case 3: NIIDMIX_BIGREG(3, 32, 4); break; case 4: NIIDMIX_BIGREG(4, 32, 4); break;
-                default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
-                }
-            }
-#undef NIIDMIX_BIGREG
-            return check_launch("k_mix_bigclique_reg");
-        }
+        if (!big_env && plan->max_clique <= 2 * kBigRegWaves * 32)
+            return launch_bigclique_reg(x, ld_x, y, ld_y, p, plan, 62, 0, 0, s);
         int waves = 8, bpc = 16;
         if (big_env) sscanf(big_env, "%dx%d", &waves, &bpc);
         if (bpc < 1) bpc = 1;

@@ -420,8 +420,9 @@ class Mixer:
         _req(mode == "fast" and kernel in (None, "clique"),
              "blocked slabs: only the clique kernel (fast mode) reads the blocked layout")
         _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
-        _req(self.plan.max_clique <= 256, "blocked slabs: cliques of <= 256 members (register "
-             "tile); a bigger clique (fully-connected) uses the two-pass kernel on [N, P] slabs")
+        _req(self.plan.max_clique <= 1024, "blocked slabs: cliques of <= 1024 members (register "
+             "tile, or the one-pass big-clique kernel); a bigger clique uses the two-pass kernel "
+             "on [N, P] slabs")
         mix_clique_blocked(x, self.p_clique_ptr, self.p_member_row, self.p_member_group,
                            self.p_coef, self.p_res_ptr, self.p_res_col, self.p_res_val,
                            self.p_res_member, out, int(p), self.plan.max_clique,

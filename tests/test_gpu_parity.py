@@ -371,3 +371,22 @@ def test_bigclique_one_pass(n, size, inter, p, gpu, oracle_mod, monkeypatch):
     ok, worst = oracle_mod.check_tolerance(y2, ref, bound, rtol=RTOL)
     assert ok, worst
     assert np.max(np.abs(y - y2)) <= 1e-5 * np.max(bound)
+
+
+@pytest.mark.parametrize("n,size,inter", [(1000, 1000, "ring"), (1200, 600, "ring"), (2000, 500, "smallworld")])
+def test_bigclique_blocked_layout(n, size, inter, gpu):
+    """The one-pass big-clique kernel on column-blocked slabs [P/B, N, B] (B = 256 and 1024, a
+    ragged last block) is bit-identical to the same kernel on the row-major slab."""
+    from niidmix import memory, ops
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(n, size, inter, 1337)
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.plan is not None and m.plan.max_clique > 256, m.plan_reason
+    for p, bc in ((1500, 256), (2048 + 96, 1024)):
+        gen = torch.Generator().manual_seed(p)
+        x = torch.randn(n, p, generator=gen).to(gpu)
+        y = m(x, kernel="clique")
+        xb = memory.to_blocked(x, bc)
+        yb = memory.empty_blocked(n, p, gpu, bc)
+        m.mix_blocked(xb, yb, p)
+        assert torch.equal(memory.from_blocked(yb, p), y)
