@@ -719,7 +719,7 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8,
-    int bc_shift, int64_t bs_x, int64_t bs_y) {
+    int bc_shift, int64_t bs_x, int64_t bs_y, int contig) {
     // column c of row r: x[(c >> bc_shift) * bs_x + r * ld_x + (c & (2^bc_shift - 1))] -- the
     // column-blocked layout [P / B, N, B] (ld = B), or row-major with bc_shift = 62, bs = 0
     constexpr int MMAX = kBigRegWaves * 2 * R;
@@ -737,7 +737,9 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
         const int64_t xcd = t & 7;
         const int64_t local = t >> 3;
         const int32_t cq = (int32_t)(local / nch8);
-        const int64_t chunk = (local % nch8) * 8 + xcd;
+        // contig: XCD x owns chunks [x*nch8, (x+1)*nch8), so the items one XCD runs together read
+        // neighbouring 128-B pieces of the same rows; else chunks interleave over the XCDs
+        const int64_t chunk = contig ? xcd * nch8 + local % nch8 : (local % nch8) * 8 + xcd;
         const int64_t c0 = chunk * kBigRegCols;
         if (c0 >= p) continue;                               // block-uniform
         if (cq != cur) {                                     // block-uniform
@@ -1651,10 +1653,15 @@ static int launch_bigclique_reg(const float *x, int64_t ld_x, float *y, int64_t 
     const int64_t items = (int64_t)plan->n_cliques * nch8 * 8;
     const bool r16 = plan->max_clique <= 2 * kBigRegWaves * 16;
     const int bpc = (r16 || plan->n_groups == 1) ? 2 : 1;
+    // item map, measured on FC-1000 (tools/s74.sh, one box): row-major slabs contiguous chunk
+    // ranges per XCD 1.85 ms vs 2.02 ms interleaved; column-blocked slabs interleaved 1.70 ms vs
+    // 1.73 ms.  NIIDMIX_BIGREG_MAP=interleave|contig overrides (A/B).
+    const char *map_env = getenv("NIIDMIX_BIGREG_MAP");
+    const int contig = map_env ? (!strcmp(map_env, "contig") ? 1 : 0) : (bc_shift >= 62 ? 1 : 0);
     int64_t gsz = (int64_t)bpc * cu_count();
     if (gsz > items) gsz = items;
     const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
-#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y)
+#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y, contig)
     if (r16) {
         switch (plan->n_groups) {
         case 1: NIIDMIX_BIGREG(1, 16, 8); break; case 2: NIIDMIX_BIGREG(2, 16, 8); break;
