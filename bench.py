@@ -60,7 +60,7 @@ def parse():
                              "dcliques10000"])
     ap.add_argument("--p", type=int, default=None, help="parameters per node (default per config)")
     ap.add_argument("--kernel", default="auto",
-                    choices=["auto", "csr-exact", "csr-fast", "clique", "dense", "staged-exact", "staged-fast", "tile-exact", "tile-fast", "tile-lds-exact", "tile-lds-fast"])
+                    choices=["auto", "csr-exact", "csr-fast", "clique", "dense", "tile-exact", "tile-fast", "tile-lds-exact", "tile-lds-fast"])
     ap.add_argument("--interclique", default="fully-connected",
                     choices=["fully-connected", "smallworld", "ring"],
                     help="multi-GPU global d-cliques interclique topology")

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NIIDMIX_ABI_VERSION 1
+#define NIIDMIX_ABI_VERSION 2
 
 enum niidmix_status {
     NIIDMIX_OK = 0,
@@ -117,7 +117,14 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
  *                big-clique kernel (a 32-column item of every member held in registers, one HBM
  *                read per parameter); larger cliques a two-pass kernel (rows read twice)
  *   max_clique_res  largest number of residual terms of one clique (informational, >= 0)
- *   n_groups     1..4 */
+ *   n_groups     1..4
+ *   csr_ptr / csr_col / csr_val   the CSR of the same W^T (niidmix_mix_csr_f32's row_ptr / col /
+ *                val, rows indexed like member_row): the non-finite guard.  The factored form
+ *                combines every member into every output, the reference only a node's real edges
+ *                (d_sgd.py:105-106) on top of self*0 (model/__init__.py:20-21); every output the
+ *                kernel finds non-finite is recomputed from its CSR row (fast-mode arithmetic), so
+ *                inf / NaN propagate exactly along real edges and a non-finite self gives NaN.
+ * Range checks: x and y must not overlap over the member rows (NIIDMIX_EALIAS). */
 #define NIIDMIX_MEMBER_GATEWAY 256
 
 typedef struct niidmix_clique_plan {
@@ -134,34 +141,13 @@ typedef struct niidmix_clique_plan {
     const int32_t *res_col;
     const float *res_val;
     const int32_t *res_member;
+    const int64_t *csr_ptr;
+    const int32_t *csr_col;
+    const float *csr_val;
 } niidmix_clique_plan;
 
 int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                            const niidmix_clique_plan *plan, void *stream);
-
-/* Block-staged CSR mixing, exact or fast: the same result as niidmix_mix_csr_f32 (bit for bit in
- * NIIDMIX_MODE_EXACT: same per-row operand order and roundings) with the gathers served from LDS.
- * Output rows are grouped into blocks (e.g. the cliques); each block lists its distinct source rows
- * (<= 256), and scol gives, for every CSR entry, the slot of its source in its row's block.
- *   blk_ptr  [n_blocks+1] int32 offsets into blk_rows; blk_rows: output rows (each exactly once)
- *   src_ptr  [n_blocks+1] int32 offsets into src_rows; src_rows: input rows staged per block
- *   row_ptr / val        the CSR of niidmix_mix_csr_f32 (int64 / fp32)
- *   scol     [nnz] int32 slot (index into the block's source list) of every CSR entry
- *   max_src  largest source list (selects the LDS footprint) */
-typedef struct niidmix_staged_plan {
-    int32_t n_blocks;
-    int32_t max_src;
-    const int32_t *blk_ptr;
-    const int32_t *blk_rows;
-    const int32_t *src_ptr;
-    const int32_t *src_rows;
-    const int64_t *row_ptr;
-    const int32_t *scol;
-    const float *val;
-} niidmix_staged_plan;
-
-int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                           const niidmix_staged_plan *plan, int mode, void *stream);
 
 /* The same clique-factored round on COLUMN-BLOCKED slabs: x and y are [K][rows][block_cols]
  * (K = ceil(p / block_cols) blocks of row-major [rows, block_cols] sub-slabs with row stride `ld`
@@ -246,9 +232,13 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
  * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).
  *   w  [n, n] fp32 row-major, w[src*n + dst] = W[src, dst] — the reference's topology['weights']
  *      layout (topology/__init__.py:9) — device pointer
- *   x  [n, ld_x], y [n, ld_y] */
+ *   x  [n, ld_x], y [n, ld_y]
+ *   row_ptr / col / val   the CSR of the same W^T (as niidmix_mix_csr_f32): the non-finite guard
+ *      (see niidmix_clique_plan.csr_ptr) — an output the GEMM finds non-finite (W = 0 off the edges
+ *      gives 0*inf = NaN) is recomputed from its node's real edges. */
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
-                          int64_t p, const float *w, void *stream);
+                          int64_t p, const float *w, const int64_t *row_ptr, const int32_t *col,
+                          const float *val, void *stream);
 
 /* Column mean over rows (the uniform global average of setup.model.average(models) with
  * weights=None, model/__init__.py:17-18, used by d_sgd.init :137-141 and the logger :112,260),

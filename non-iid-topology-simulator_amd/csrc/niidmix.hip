@@ -97,6 +97,62 @@ __device__ __forceinline__ float4 axpy4(float w, float4 xv, float4 acc) {
 }
 
 // ----------------------------------------------------------------------------------------------
+// Non-finite guard of the factored and GEMM kernels (fast mode).  The reference sums only over a
+// node's real edges ([self] + edges[rank], d_sgd.py:105-106) on top of self*0 (model/__init__.py:
+// 20-21): a non-finite value reaches an output only along a real edge, and a non-finite SELF value
+// makes the output NaN.  The factored form a*x_i + sum_g c_g*S_g + residuals (and a GEMM with W = 0
+// off the edges) combines every clique member / every node into every output, so a non-finite x_j
+// would leak into outputs that never read it (c*inf - c*inf = NaN for a removed clique edge, 0*inf
+// = NaN in the GEMM).  Conversely a factored output is finite only if every value it combined is
+// finite.  Hence every output the fast kernel finds non-finite is recomputed from the node's CSR
+// row in the reference's operand order with fast-mode arithmetic (z = x_self*0, acc = fma(w, x_j,
+// acc), y = z + acc: k_mix_csr's fast mode), which reproduces the reference's inf / NaN pattern.
+// Finite outputs are untouched; the check costs one v_cmp_class per output element.
+//   row-uniform form (one wave, V columns per lane): csr_refix;  per-lane form: csr_refix1.
+__device__ __forceinline__ bool finite4(const float *v) {
+    return __builtin_isfinite(v[0]) & __builtin_isfinite(v[1]) & __builtin_isfinite(v[2]) &
+           __builtin_isfinite(v[3]);
+}
+
+template <int V>
+__device__ __forceinline__ void csr_refix(const float *__restrict__ xc, int64_t ld_x, unsigned lo, bool act,
+                                       int64_t row, const int64_t *__restrict__ rp,
+                                       const int32_t *__restrict__ col, const float *__restrict__ val,
+                                       float *__restrict__ o) {
+    const int64_t b = rp[row], e = rp[row + 1];
+    float z[V], acc[V];
+#pragma unroll
+    for (int c = 0; c < V; ++c) { z[c] = 0.f; acc[c] = 0.f; }
+    for (int64_t k = b; k < e; ++k) {
+        const float *src = xc + (int64_t)col[k] * ld_x + lo;
+        float xv[V];
+#pragma unroll
+        for (int c = 0; c < V; ++c) xv[c] = act ? src[c] : 0.f;
+        if (k == b) {
+#pragma unroll
+            for (int c = 0; c < V; ++c) { z[c] = xv[c] * 0.f; acc[c] = z[c]; }
+        }
+        const float w = val[k];
+#pragma unroll
+        for (int c = 0; c < V; ++c) acc[c] = __builtin_fmaf(w, xv[c], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < V; ++c) o[c] = z[c] + acc[c];
+}
+
+__device__ __forceinline__ float csr_refix1(const float *__restrict__ xc, int64_t ld_x, int64_t row,
+                                         const int64_t *__restrict__ rp,
+                                         const int32_t *__restrict__ col,
+                                         const float *__restrict__ val) {
+    const int64_t b = rp[row], e = rp[row + 1];
+    if (b == e) return 0.f;
+    const float z = xc[(int64_t)col[b] * ld_x] * 0.f;
+    float acc = z;
+    for (int64_t k = b; k < e; ++k) acc = __builtin_fmaf(val[k], xc[(int64_t)col[k] * ld_x], acc);
+    return z + acc;
+}
+
+// ----------------------------------------------------------------------------------------------
 // Generic CSR mixing.  Work item = (group of 4 output rows, chunk of 256 columns); each wave owns
 // one output row.  Work order is XCD-aware: items t and t+8 share an XCD (round-robin dispatch),
 // and consecutive items on one XCD sweep all rows of the SAME chunk, so the chunk's source rows
@@ -300,7 +356,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val,
     const int32_t *__restrict__ res_member, int64_t n_items, int64_t skew, int cpb_shift,
-    int64_t bs_x, int64_t bs_y) {
+    int64_t bs_x, int64_t bs_y, const int64_t *__restrict__ csr_ptr,
+    const int32_t *__restrict__ csr_col, const float *__restrict__ csr_val) {
     // column-blocked slabs ([K][rows][B], B = CW << cpb_shift columns, block strides bs_x / bs_y
     // floats; a row-major slab is one block: cpb_shift = 62): chunk c lives in block c >> cpb_shift
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
@@ -479,7 +536,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int e = 0; e < V; ++e) sg[g][e] = NO_RED ? red[g][wave][V * lane + e] : tot[g][V * lane + e];
-    // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here)
+    // 5. y_r = v_r + sum_g c_{r,g} S_g, each stored as soon as it is formed (no loads from here);
+    //    a row with a non-finite output (rare) is recomputed from its CSR row afterwards
+    uint32_t bad = 0;                                                    // wave-uniform row bits
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
         if (wave + WAVES * r < M) {
@@ -490,11 +549,21 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(cg, sg[g][e], v[r][e]);
             }
             const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-            if (act) {
+            if (__ballot(act && !finite4(v[r]))) {
+                bad |= 1u << r;
+            } else if (act) {
                 if (PLAIN_ST) *reinterpret_cast<float4 *>(yc + row * ld_y + lo) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
                 else stv_nt<V>(yc + row * ld_y + lo, v[r]);
             }
         }
+    }
+    while (bad) {                                                         // non-finite guard
+        const int r = __builtin_ctz(bad);
+        bad &= bad - 1;
+        const int64_t row = __builtin_amdgcn_readlane(d.row, r);
+        float o[V];
+        csr_refix<V>(xc, ld_x, lo, act, row, csr_ptr, csr_col, csr_val, o);
+        if (act) stv_nt<V>(yc + row * ld_y + lo, o);
     }
 }
 
@@ -512,7 +581,10 @@ template <bool VEC, bool AVEC>
 __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
                                                       float *__restrict__ y, int64_t ld_y, int64_t n,
                                                       int64_t p, const float *__restrict__ w,
-                                                      int64_t n_it, int64_t n_items) {
+                                                      int64_t n_it, int64_t n_items,
+                                                      const int64_t *__restrict__ csr_ptr,
+                                                      const int32_t *__restrict__ csr_col,
+                                                      const float *__restrict__ csr_val) {
     __shared__ float As[2][kDBK][kDBM + kDPad];
     __shared__ float Bs[2][kDBK][kDBN + kDPad];
     const int tid = threadIdx.x;
@@ -591,6 +663,7 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
             }
             buf ^= 1;
         }
+        uint64_t bad = 0;                         // this lane's non-finite outputs (a, b, r)
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -599,8 +672,19 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
                 for (int r = 0; r < 16; ++r) {
                     const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                     const int64_t j = j0 + wn * 64 + b * 32 + (lane & 31);
-                    if (i < n && j < p) __builtin_nontemporal_store(acc[a][b][r], y + i * ld_y + j);
+                    if (i < n && j < p) {
+                        if (__builtin_isfinite(acc[a][b][r])) __builtin_nontemporal_store(acc[a][b][r], y + i * ld_y + j);
+                        else bad |= 1ull << (a * 32 + b * 16 + r);
+                    }
                 }
+        while (bad) {                             // non-finite guard (see csr_refix): 0*inf from
+            const int q = __builtin_ctzll(bad);   // W = 0 off the edges must not leak into outputs
+            bad &= bad - 1;
+            const int a = q >> 5, b = (q >> 4) & 1, r = q & 15;
+            const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int64_t j = j0 + wn * 64 + b * 32 + (lane & 31);
+            __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
+        }
         __syncthreads();   // LDS buffers are rewritten by the next tile
     }
 }
@@ -620,7 +704,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
-    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items) {
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_items,
+    const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
+    const float *__restrict__ csr_val) {
     constexpr int U = 8;
     __shared__ float red[G][WAVES][kWave];
     const int wave = wave_id();
@@ -692,10 +778,21 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     v[u] = kn < ke ? xc[(int64_t)member_row[kn + u < ke ? kn + u : kn] * ld_x + lo] : 0.f;
+                uint32_t bad = 0;
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (k + u < ke && act)
-                        __builtin_nontemporal_store(o[u], yc + (int64_t)member_row[k + u] * ld_y + lane);
+                    if (k + u < ke && act) {
+                        if (__builtin_isfinite(o[u]))
+                            __builtin_nontemporal_store(o[u], yc + (int64_t)member_row[k + u] * ld_y + lane);
+                        else bad |= 1u << u;
+                    }
+                while (bad) {                                 // non-finite guard (see csr_refix)
+                    const int u = __builtin_ctz(bad);
+                    bad &= bad - 1;
+                    const int64_t row = member_row[k + u];
+                    __builtin_nontemporal_store(csr_refix1(xc + lo, ld_x, row, csr_ptr, csr_col, csr_val),
+                                                yc + row * ld_y + lane);
+                }
             }
         }
     }
@@ -719,7 +816,8 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
     const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
     const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
     const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8,
-    int bc_shift, int64_t bs_x, int64_t bs_y, int contig) {
+    int bc_shift, int64_t bs_x, int64_t bs_y, int contig, const int64_t *__restrict__ csr_ptr,
+    const int32_t *__restrict__ csr_col, const float *__restrict__ csr_val) {
     // column c of row r: x[(c >> bc_shift) * bs_x + r * ld_x + (c & (2^bc_shift - 1))] -- the
     // column-blocked layout [P / B, N, B] (ld = B), or row-major with bc_shift = 62, bs = 0
     constexpr int MMAX = kBigRegWaves * 2 * R;
@@ -815,101 +913,22 @@ __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_
                         v[i] = __builtin_fmaf(res_val[q], xc[(int64_t)res_col[q] * ld_x], v[i]);
             }
         }
+        uint32_t bad = 0;                                     // this lane's non-finite outputs
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int k = 2 * (wave * R + i) + h;
-            if (k < M && act) __builtin_nontemporal_store(v[i], yc + (int64_t)s_row[k] * ld_y);
-        }
-    }
-}
-
-// ----------------------------------------------------------------------------------------------
-// Block-staged CSR mixing (exact or fast).  Output rows are grouped into blocks (the cliques); a
-// block's distinct source rows (members + remote neighbours, <= 256) are staged ONCE per column
-// chunk in LDS, then every output row accumulates its CSR entries in the reference's order from
-// LDS.  HBM traffic ~ 2*4 B per node-parameter (+ remote rows), the gathers hit LDS instead of L2:
-// the exact mode's bound moves from L2 bandwidth (k_mix_csr) to LDS/VALU.
-// Chunk = 64 lanes x VPL floats.  Per-entry slot/weight are wave-uniform -> scalar loads.
-template <bool EXACT, int VPL>
-__global__ __launch_bounds__(256) void k_mix_staged(
-    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
-    int32_t n_blocks, const int32_t *__restrict__ blk_ptr, const int32_t *__restrict__ blk_rows,
-    const int32_t *__restrict__ src_ptr, const int32_t *__restrict__ src_rows,
-    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ scol,
-    const float *__restrict__ val, int64_t n_items, int avg_only) {
-    extern __shared__ __attribute__((aligned(16))) float stage[];   // [n_src][64 * VPL]
-    constexpr int CW = 64 * VPL;
-    const int wave = wave_id();
-    const int lane = threadIdx.x & (kWave - 1);
-    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
-        const int64_t xcd = t & 7;
-        const int64_t local = t >> 3;
-        const int64_t chunk = (local / n_blocks) * 8 + xcd;
-        const int32_t b = (int32_t)(local % n_blocks);
-        const int64_t c0 = chunk * CW;
-        if (c0 >= p) continue;                              // block-uniform
-        const int64_t c = c0 + VPL * lane;
-        const bool act = c < p;                             // p % VPL == 0
-        const int32_t s0 = src_ptr[b], ns = src_ptr[b + 1] - s0;
-        // 1. stage the block's source rows (each wave a share of the rows, one row per instruction)
-        for (int32_t r = wave; r < ns; r += 4) {
-            const float *src = x + (int64_t)src_rows[s0 + r] * ld_x;
-            float v[VPL];
-#pragma unroll
-            for (int e = 0; e < VPL; ++e) v[e] = 0.f;
-            if (act) ldv<VPL>(src + c, v);
-#pragma unroll
-            for (int e = 0; e < VPL; ++e) stage[r * CW + VPL * lane + e] = v[e];
-        }
-        __syncthreads();
-        // 2. every output row of the block, entries in CSR order, operands from LDS
-        const int32_t r0 = blk_ptr[b], nr = blk_ptr[b + 1] - r0;
-        for (int32_t i = wave; i < nr; i += 4) {
-            const int64_t row = blk_rows[r0 + i];
-            const int64_t beg = row_ptr[row], end = row_ptr[row + 1];
-            float z[VPL], acc[VPL];
-            {
-                const float *sp = stage + (int64_t)scol[beg] * CW + VPL * lane;
-#pragma unroll
-                for (int e = 0; e < VPL; ++e) { z[e] = sp[e] * 0.f; acc[e] = z[e]; }
-            }
-            // entry descriptors 64 at a time, lane-parallel (one vector load each), handed to the
-            // scalar unit by v_readlane: no scalar-load latency inside the accumulation chain
-            constexpr int U = 8;   // U LDS reads in flight, then in-order accumulation
-            for (int64_t kb = beg; kb < end; kb += 64) {
-                const int cnt = (int)(end - kb < 64 ? end - kb : 64);
-                const int d_s = lane < cnt ? scol[kb + lane] : 0;
-                const float d_w = lane < cnt ? val[kb + lane] : 0.f;
-                for (int j = 0; j < cnt; j += U) {
-                    float xv[U][VPL];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int slot = __builtin_amdgcn_readlane(d_s, j + u < cnt ? j + u : 0);
-                        const float *sp = stage + slot * CW + VPL * lane;
-                        if (VPL == 2) {
-                            const float2 t2 = *reinterpret_cast<const float2 *>(sp);
-                            xv[u][0] = t2.x; xv[u][VPL - 1] = t2.y;
-                        } else {
-                            xv[u][0] = sp[0];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (j + u < cnt) {
-                            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_w), j + u));
-#pragma unroll
-                            for (int e = 0; e < VPL; ++e) acc[e] = axpy<EXACT>(w, xv[u][e], acc[e]);
-                        }
-                }
-            }
-            if (act) {
-                float o[VPL];
-#pragma unroll
-                for (int e = 0; e < VPL; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
-                stv_nt<VPL>(y + row * ld_y + c, o);
+            if (k < M && act) {
+                if (__builtin_isfinite(v[i])) __builtin_nontemporal_store(v[i], yc + (int64_t)s_row[k] * ld_y);
+                else bad |= 1u << i;
             }
         }
-        __syncthreads();                                    // stage[] is refilled by the next item
+        while (bad) {                                         // non-finite guard (see csr_refix)
+            const int i = __builtin_ctz(bad);
+            bad &= bad - 1;
+            const int64_t row = s_row[2 * (wave * R + i) + h];
+            __builtin_nontemporal_store(csr_refix1(xc, ld_x, row, csr_ptr, csr_col, csr_val),
+                                        yc + row * ld_y);
+        }
     }
 }
 
@@ -1423,7 +1442,7 @@ void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
                        pl->res_val, pl->res_member, n_items, clique_skew(), bg.cpb_shift, bg.bs_x,
-                       bg.bs_y);
+                       bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val);
 }
 
 template <int WAVES, int RPW, int OCC, int RW, int FL, int V>
@@ -1602,7 +1621,7 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     if (n_rows == 0 || p == 0) return NIIDMIX_OK;
     if (!x || !y || !row_ptr || !col || !val) return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (x == y || (x > y && x < y + (n_rows - 1) * ld_y + p))
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
@@ -1661,7 +1680,7 @@ static int launch_bigclique_reg(const float *x, int64_t ld_x, float *y, int64_t 
     int64_t gsz = (int64_t)bpc * cu_count();
     if (gsz > items) gsz = items;
     const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
-#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y, contig)
+#define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y, contig, plan->csr_ptr, plan->csr_col, plan->csr_val)
     if (r16) {
         switch (plan->n_groups) {
         case 1: NIIDMIX_BIGREG(1, 16, 8); break; case 2: NIIDMIX_BIGREG(2, 16, 8); break;
@@ -1688,14 +1707,20 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
     if (plan->n_cliques == 0 || p == 0) return NIIDMIX_OK;
     if (!x || !y || !plan->clique_ptr || !plan->member_row || !plan->member_group || !plan->coef ||
         !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
-        (!plan->res_member && plan->n_members > 0))
+        (!plan->res_member && plan->n_members > 0) || !plan->csr_ptr || !plan->csr_col || !plan->csr_val)
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (block_cols < 256 || (block_cols & (block_cols - 1)))
         return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= 256", (long long)block_cols);
     if (ld < block_cols) return set_error(NIIDMIX_EINVAL, "row stride < block_cols");
     if (block_stride_x < ld || block_stride_y < ld)
         return set_error(NIIDMIX_EINVAL, "block stride < row stride");
-    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    {   // extents of the member rows in both slabs (x may hold more rows: halo rows of a shard)
+        const int64_t k_blocks = (p + block_cols - 1) / block_cols;
+        const int64_t rows = plan->n_members > 0 ? plan->n_members : 1;
+        if (overlaps(x, (k_blocks - 1) * block_stride_x + (rows - 1) * ld + block_cols,
+                     y, (k_blocks - 1) * block_stride_y + (rows - 1) * ld + block_cols))
+            return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    }
     if (plan->max_clique > 2 * kBigRegWaves * 32)
         return set_error(NIIDMIX_EUNSUPPORTED, "blocked slabs: cliques of <= 1024 members");
     if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
@@ -1720,10 +1745,14 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     if (plan->n_cliques == 0 || p == 0) return NIIDMIX_OK;
     if (!x || !y || !plan->clique_ptr || !plan->member_row || !plan->member_group || !plan->coef ||
         !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
-        (!plan->res_member && plan->n_members > 0))
+        (!plan->res_member && plan->n_members > 0) || !plan->csr_ptr || !plan->csr_col || !plan->csr_val)
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    {   // extents of the member rows in both slabs (x may hold more rows: halo rows of a shard)
+        const int64_t rows = plan->n_members > 0 ? plan->n_members : 1;
+        if (overlaps(x, (rows - 1) * ld_x + p, y, (rows - 1) * ld_y + p))
+            return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    }
     if (plan->max_clique_res < 0) return set_error(NIIDMIX_EINVAL, "negative max_clique_res");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool vec4 = (p % 4 == 0) && (ld_x % 4 == 0) && (ld_y % 4 == 0) && aligned16(x) && aligned16(y);
@@ -1752,7 +1781,7 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         if (gsz > items) gsz = items;
         const dim3 grid((unsigned)gsz), block(waves * 64);
         const size_t lds = 0;
-#define NIIDMIX_BIG(G, W) hipLaunchKernelGGL((k_mix_bigclique<G, W>), grid, block, lds, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, items)
+#define NIIDMIX_BIG(G, W) hipLaunchKernelGGL((k_mix_bigclique<G, W>), grid, block, lds, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, items, plan->csr_ptr, plan->csr_col, plan->csr_val)
 #define NIIDMIX_BIGW(W) switch (plan->n_groups) { case 1: NIIDMIX_BIG(1, W); break; case 2: NIIDMIX_BIG(2, W); break; case 3: NIIDMIX_BIG(3, W); break; case 4: NIIDMIX_BIG(4, W); break; default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups); }
         if (waves == 4) { NIIDMIX_BIGW(4); }
         else if (waves == 8) { NIIDMIX_BIGW(8); }
@@ -1762,37 +1791,6 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
         return check_launch("k_mix_bigclique");
     }
     return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, vec4, s);
-}
-
-int niidmix_mix_staged_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                           const niidmix_staged_plan *plan, int mode, void *stream) {
-    if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
-    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
-    mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
-    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
-        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
-    if (p < 0 || plan->n_blocks < 0) return set_error(NIIDMIX_EINVAL, "negative size");
-    if (plan->n_blocks == 0 || p == 0) return NIIDMIX_OK;
-    if (!x || !y || !plan->blk_ptr || !plan->blk_rows || !plan->src_ptr || !plan->src_rows ||
-        !plan->row_ptr || !plan->scol || !plan->val)
-        return set_error(NIIDMIX_EINVAL, "null pointer");
-    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
-    if (plan->max_src < 1 || plan->max_src > 256)
-        return set_error(NIIDMIX_EUNSUPPORTED, "block with %d source rows (1..256 supported)", plan->max_src);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
-    const int vpl = (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0 && plan->max_src <= 160) ? 2 : 1;
-    const int64_t cw = 64 * vpl;
-    const int64_t n_chunks = (p + cw - 1) / cw;
-    const int64_t n_items = (int64_t)plan->n_blocks * ((n_chunks + 7) / 8) * 8;
-    const size_t lds = (size_t)plan->max_src * cw * sizeof(float);
-    const dim3 grid((unsigned)grid_for(n_items)), block(256);
-#define NIIDMIX_STAGED(E, V) hipLaunchKernelGGL((k_mix_staged<E, V>), grid, block, lds, s, x, ld_x, y, ld_y, p, plan->n_blocks, plan->blk_ptr, plan->blk_rows, plan->src_ptr, plan->src_rows, plan->row_ptr, plan->scol, plan->val, n_items, avg_only)
-    if (mode == NIIDMIX_MODE_EXACT) { if (vpl == 2) NIIDMIX_STAGED(true, 2); else NIIDMIX_STAGED(true, 1); }
-    else                            { if (vpl == 2) NIIDMIX_STAGED(false, 2); else NIIDMIX_STAGED(false, 1); }
-#undef NIIDMIX_STAGED
-    return check_launch("k_mix_staged");
 }
 
 int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
@@ -1885,10 +1883,11 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
 }
 
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
-                          int64_t p, const float *w, void *stream) {
+                          int64_t p, const float *w, const int64_t *row_ptr, const int32_t *col,
+                          const float *val, void *stream) {
     if (n < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
     if (n == 0 || p == 0) return NIIDMIX_OK;
-    if (!x || !y || !w) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (!x || !y || !w || !row_ptr || !col || !val) return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
     if (overlaps(x, (n - 1) * ld_x + p, y, (n - 1) * ld_y + p))
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
@@ -1899,7 +1898,7 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
     const dim3 grid((unsigned)grid_for(n_items)), block(256);
     const bool avec = (n % 4 == 0) && aligned16(w);
-#define NIIDMIX_DENSE(V, A) hipLaunchKernelGGL((k_mix_dense<V, A>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items)
+#define NIIDMIX_DENSE(V, A) hipLaunchKernelGGL((k_mix_dense<V, A>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items, row_ptr, col, val)
     if (vec) { if (avec) NIIDMIX_DENSE(true, true); else NIIDMIX_DENSE(true, false); }
     else     { if (avec) NIIDMIX_DENSE(false, true); else NIIDMIX_DENSE(false, false); }
 #undef NIIDMIX_DENSE

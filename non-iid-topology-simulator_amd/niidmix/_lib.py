@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NIIDMIX_LIB", os.path.join(_HERE, "libniidmix.so"))
 
 OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
 MODE_EXACT, MODE_FAST = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
 
@@ -26,13 +26,8 @@ class CliquePlanC(ctypes.Structure):
     """Mirror of struct niidmix_clique_plan (include/niidmix.h)."""
     _fields_ = [("n_cliques", _i32), ("n_members", _i32), ("n_groups", _i32), ("max_clique", _i32),
                 ("max_clique_res", _i32), ("clique_ptr", _vp), ("member_row", _vp), ("member_group", _vp), ("coef", _vp),
-                ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp), ("res_member", _vp)]
-
-
-class StagedPlanC(ctypes.Structure):
-    """Mirror of struct niidmix_staged_plan (include/niidmix.h)."""
-    _fields_ = [("n_blocks", _i32), ("max_src", _i32), ("blk_ptr", _vp), ("blk_rows", _vp),
-                ("src_ptr", _vp), ("src_rows", _vp), ("row_ptr", _vp), ("scol", _vp), ("val", _vp)]
+                ("res_ptr", _vp), ("res_col", _vp), ("res_val", _vp), ("res_member", _vp),
+                ("csr_ptr", _vp), ("csr_col", _vp), ("csr_val", _vp)]
 
 
 class TilePlanC(ctypes.Structure):
@@ -59,13 +54,12 @@ SIGNATURES = {
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                                       ctypes.POINTER(CliquePlanC), _vp]),
-    "niidmix_mix_staged_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
-                                              ctypes.POINTER(StagedPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                             ctypes.POINTER(TilePlanC), ctypes.c_int, _vp]),
     "niidmix_mix_tile_lds_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                                 ctypes.POINTER(TileLdsPlanC), ctypes.c_int, _vp]),
-    "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
+                                             _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp,
                                                      _vp]),

@@ -40,6 +40,10 @@ class CliquePlan:
     res_col: np.ndarray        # int32 [R]
     res_val: np.ndarray        # fp32 [R]
     res_member: np.ndarray = None   # int32 [R]: the entry's member index within its clique
+    n_cancel: int = 0          # residual terms that cancel (most of) a class value: removed clique
+                               # edges (-c_g) or in-clique weights far below their class value.
+                               # Their rounding error is not bounded by the row's own terms, so
+                               # Mixer's auto choice avoids the factored kernel when n_cancel > 0.
 
     @property
     def n_cliques(self):
@@ -136,6 +140,7 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
     coef = np.zeros((M, 1 + G), np.float32)
     res_ptr = np.zeros(M + 1, np.int64)
     res_cols, res_vals, res_member = [], [], []
+    n_cancel = 0
     member_row = flat.astype(np.int32)
     member_group = group_of[flat].astype(np.int32)
     clique_ptr = np.cumsum([0] + [len(c) for c in cliques]).astype(np.int32)
@@ -157,17 +162,21 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
         coef[m, 1:] = cs.astype(np.float32)
         coef[m, 0] = np.float32(w_self - float(np.float32(cs[group_of[i]])))
         rc, rv = [], []
-        # inter-clique terms
+        # inter-clique terms (zero weights kept: the reference still multiplies them, so a
+        # non-finite source gives NaN there, and the kernel's non-finite guard must see that row)
         out = ~same & (cols != i)
         for j, w in zip(cols[out], vals[out]):
-            if w != 0.0:
-                rc.append(j); rv.append(float(w))
-        # in-clique corrections (weights that differ from their class value)
+            rc.append(j); rv.append(float(w))
+        # in-clique corrections (weights that differ from their class value); one that cancels
+        # most of its class value (|w| < |c|/64) loses the fp32 accuracy of the term it replaces
         for j, w in zip(cols[same], vals[same]):
             c_j = float(np.float32(cs[group_of[j]]))
             if float(w) != c_j:
                 rc.append(j); rv.append(float(w) - c_j)
-        # in-clique members with no edge (W = 0) whose class value is not 0
+                if abs(float(w)) * 64.0 < abs(c_j):
+                    n_cancel += 1
+        # in-clique members with no edge (W = 0) whose class value is not 0: a removed clique edge
+        # (d_cliques/utils.py remove_clique_edges), corrected by -c_g (a cancelling term)
         present_set = set(cols[same].tolist())
         for g, gm in enumerate(groups):
             c_g = float(np.float32(cs[g]))
@@ -176,6 +185,7 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
             for j in gm:
                 if j != i and j not in present_set:
                     rc.append(int(j)); rv.append(-c_g)
+                    n_cancel += 1
         res_cols.extend(rc)
         res_vals.extend(rv)
         res_member.extend([m - int(clique_ptr[ci])] * len(rc))
@@ -191,5 +201,5 @@ def build_clique_plan(csr, cliques, max_res_per_node=1.0, max_groups=MAX_GROUPS,
                       res_ptr=res_ptr.astype(np.int32),
                       res_col=np.asarray(res_cols, np.int32),
                       res_val=np.asarray(res_vals, np.float64).astype(np.float32),
-                      res_member=np.asarray(res_member, np.int32))
+                      res_member=np.asarray(res_member, np.int32), n_cancel=n_cancel)
     return plan, None

@@ -2,11 +2,14 @@
 
 Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
-  mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, res_member, out,
-             max_clique, max_clique_res)            k_mix_clique_wave (fast, HBM-bound)
+  mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, res_member,
+             row_ptr, col, val, out, max_clique, max_clique_res)
+                                                    k_mix_clique (fast, HBM-bound; the CSR is the
+                                                    non-finite guard, include/niidmix.h)
+  mix_clique_blocked(..., out, p, ...)              the same on column-blocked slabs
   mix_tile_lds(x, <tile lds plan tensors>, out, rt, max_src, max_tiles, mode)
                                                     k_mix_tile_lds (exact default, LDS-staged)
-  mix_dense(x, w, out)                              k_mix_dense  (fp32 MFMA)
+  mix_dense(x, w, row_ptr, col, val, out)           k_mix_dense  (fp32 MFMA; CSR = non-finite guard)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
   grad_segment_mean(g, seg_ptr, seg_row, out)       k_grad_segment_mean (clique gradient mean)
   sgd_step_rows(p, g, rows, neg_lr)                 k_sgd_step_rows (the optimizer step, fused round)
@@ -23,7 +26,6 @@ import torch
 
 from . import _lib
 from .factor import build_clique_plan
-from .staged import build_staged_plan
 from .tile import LDS_MAX_WAVES, build_tile_lds_plan, build_tile_plan
 from .topology import MixCSR, to_csr
 
@@ -100,21 +102,25 @@ def mix_csr(x: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor, val: torc
 def mix_clique(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
                member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
                res_col: torch.Tensor, res_val: torch.Tensor, res_member: torch.Tensor,
+               row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
                out: torch.Tensor, max_clique: int, max_clique_res: int) -> None:
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     _req(member_row.device == x.device, "plan and slabs must be on the same device")
     _no_overlap(x, out)
     plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
-                          res_member, max_clique, max_clique_res)
+                          res_member, row_ptr, col, val, max_clique, max_clique_res)
     rc = _lib.lib.niidmix_mix_clique_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
                                          ctypes.byref(plan), _stream(x))
     _lib.check(rc, "niidmix::mix_clique")
 
 
 def _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
-                   res_member, max_clique, max_clique_res):
+                   res_member, row_ptr, col, val, max_clique, max_clique_res):
     dev = member_row.device
+    _vec("row_ptr", row_ptr, torch.int64, dev, member_row.numel() + 1)
+    _vec("col", col, torch.int32, dev)
+    _vec("val", val, torch.float32, dev, col.numel())
     _vec("clique_ptr", clique_ptr, torch.int32, dev)
     m = member_row.numel()
     _vec("member_row", member_row, torch.int32, dev)
@@ -133,13 +139,14 @@ def _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col,
                             res_ptr.data_ptr(), res_col.data_ptr() if res_col.numel() else
                             res_ptr.data_ptr(), res_val.data_ptr() if res_val.numel() else
                             coef.data_ptr(), res_member.data_ptr() if res_member.numel() else
-                            res_ptr.data_ptr())
+                            res_ptr.data_ptr(), row_ptr.data_ptr(), col.data_ptr(), val.data_ptr())
 
 
 @torch.library.custom_op("niidmix::mix_clique_blocked", mutates_args=("out",))
 def mix_clique_blocked(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: torch.Tensor,
                        member_group: torch.Tensor, coef: torch.Tensor, res_ptr: torch.Tensor,
                        res_col: torch.Tensor, res_val: torch.Tensor, res_member: torch.Tensor,
+                       row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
                        out: torch.Tensor, p: int, max_clique: int, max_clique_res: int) -> None:
     """Clique-factored round on column-blocked slabs x, out: [K, rows, B] (niidmix.memory)."""
     for name, t in (("x", x), ("out", out)):
@@ -152,36 +159,11 @@ def mix_clique_blocked(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: to
     _req(member_row.device == x.device, "plan and slabs must be on the same device")
     _req(x.data_ptr() != out.data_ptr(), "x and out overlap: mixing is out-of-place")
     plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
-                          res_member, max_clique, max_clique_res)
+                          res_member, row_ptr, col, val, max_clique, max_clique_res)
     rc = _lib.lib.niidmix_mix_clique_blocked_f32(x.data_ptr(), out.data_ptr(), int(p), x.stride(1),
                                                  b, x.stride(0), out.stride(0),
                                                  ctypes.byref(plan), _stream(x))
     _lib.check(rc, "niidmix::mix_clique_blocked")
-
-
-@torch.library.custom_op("niidmix::mix_staged", mutates_args=("out",))
-def mix_staged(x: torch.Tensor, blk_ptr: torch.Tensor, blk_rows: torch.Tensor,
-               src_ptr: torch.Tensor, src_rows: torch.Tensor, row_ptr: torch.Tensor,
-               scol: torch.Tensor, val: torch.Tensor, out: torch.Tensor, max_src: int,
-               mode: int) -> None:
-    _slab("x", x)
-    _slab("out", out, cols=x.shape[1])
-    dev = x.device
-    nb = blk_ptr.numel() - 1
-    _vec("blk_ptr", blk_ptr, torch.int32, dev)
-    _vec("blk_rows", blk_rows, torch.int32, dev, out.shape[0])
-    _vec("src_ptr", src_ptr, torch.int32, dev, nb + 1)
-    _vec("src_rows", src_rows, torch.int32, dev)
-    _vec("row_ptr", row_ptr, torch.int64, dev, out.shape[0] + 1)
-    _vec("scol", scol, torch.int32, dev)
-    _vec("val", val, torch.float32, dev, scol.numel())
-    _no_overlap(x, out)
-    plan = _lib.StagedPlanC(nb, int(max_src), blk_ptr.data_ptr(), blk_rows.data_ptr(),
-                            src_ptr.data_ptr(), src_rows.data_ptr(), row_ptr.data_ptr(),
-                            scol.data_ptr(), val.data_ptr())
-    rc = _lib.lib.niidmix_mix_staged_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
-                                         ctypes.byref(plan), int(mode), _stream(x))
-    _lib.check(rc, "niidmix::mix_staged")
 
 
 @torch.library.custom_op("niidmix::mix_tile", mutates_args=("out",))
@@ -244,15 +226,20 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
 
 
 @torch.library.custom_op("niidmix::mix_dense", mutates_args=("out",))
-def mix_dense(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
+def mix_dense(x: torch.Tensor, w: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor,
+              val: torch.Tensor, out: torch.Tensor) -> None:
     _slab("x", x)
     n = x.shape[0]
     _slab("out", out, rows=n, cols=x.shape[1])
     _req(w.device == x.device and w.dtype == torch.float32 and w.shape == (n, n) and
          w.is_contiguous(), "w: expected contiguous fp32 [N, N] (W[src, dst])")
+    _vec("row_ptr", row_ptr, torch.int64, x.device, n + 1)
+    _vec("col", col, torch.int32, x.device)
+    _vec("val", val, torch.float32, x.device, col.numel())
     _no_overlap(x, out)
     rc = _lib.lib.niidmix_mix_dense_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n,
-                                        x.shape[1], w.data_ptr(), _stream(x))
+                                        x.shape[1], w.data_ptr(), row_ptr.data_ptr(),
+                                        col.data_ptr(), val.data_ptr(), _stream(x))
     _lib.check(rc, "niidmix::mix_dense")
 
 
@@ -320,14 +307,32 @@ def sgd_step_rows(p: torch.Tensor, g: torch.Tensor, rows: torch.Tensor, neg_lr: 
 
 
 # ------------------------------------------------------------------------------------------------
+# Mixer attributes built on first use (plan group -> attributes it sets)
+_LAZY = {
+    "plan": "clique", "plan_reason": "clique", "p_clique_ptr": "clique", "p_member_row": "clique",
+    "p_member_group": "clique", "p_coef": "clique", "p_res_ptr": "clique", "p_res_col": "clique",
+    "p_res_val": "clique", "p_res_member": "clique",
+    "tile": "tile", "tile_reason": "tile", "t_sub_ptr": "tile", "t_sub_rows": "tile",
+    "t_sub_wself": "tile", "t_pos_src": "tile", "t_pos_mask": "tile", "t_pos_w": "tile",
+    "tlds": "tlds", "tlds_reason": "tlds", "l_sub_ptr": "tlds", "l_sub_rows": "tlds",
+    "l_sub_slot": "tlds", "l_sub_wself": "tlds", "l_pos_slot": "tlds", "l_pos_mask": "tlds",
+    "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
+    "w_dense": "dense",
+}
+
+
 class Mixer:
     """One topology's mixing operator on one device: Θ' = Wᵀ Θ for a [N, P] fp32 slab.
 
     kernel='auto' picks (fast mode):  clique-factored if W factors exactly over its cliques
-    (factor.py; a fully-connected topology counts as one clique), else dense MFMA if W is a genuinely
-    dense GEMM (nnz >= dense_threshold * N^2), else the CSR gather.  mode='exact' uses the CSR kernel
-    (kernel='staged-exact' selects the LDS-staged variant); both follow the reference's operand
-    order bit for bit.
+    (factor.py; a fully-connected topology counts as one clique) without cancelling correction
+    terms, else dense MFMA if W is a genuinely dense GEMM (nnz >= dense_threshold * N^2), else the
+    LDS-staged tiles where the plan has cancelling corrections (removed clique edges), else the CSR
+    gather.  mode='exact' uses the LDS-staged merged-order tiles where they build, else the global
+    tiles, else the CSR gather; all follow the reference's operand order bit for bit.
+
+    Plans are built on first use of the kernel that needs them (a random-graph round that only
+    mixes in exact mode never builds the clique plan or a dense W).
     """
 
     def __init__(self, topology=None, *, csr=None, cliques=None, device="cuda",
@@ -338,81 +343,106 @@ class Mixer:
             cliques = topology.get("cliques")
         self.csr = csr
         self.n = csr.n
+        self.cliques = cliques
         self.device = torch.device(device)
+        self.factor = factor
         dev = self.device
+        # the CSR is always on the device: the gather kernels read it and the factored / GEMM
+        # kernels recompute non-finite outputs from it (include/niidmix.h)
         self.row_ptr = torch.from_numpy(csr.row_ptr).to(dev)
         self.col = torch.from_numpy(csr.col).to(dev)
         self.val = torch.from_numpy(csr.val).to(dev)
+        self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
+                      and self.n >= 64)
+
+    def __getattr__(self, name):
+        group = _LAZY.get(name)
+        if group is None:
+            raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
+        getattr(self, "_build_" + group)()
+        return self.__dict__[name]
+
+    def _build_clique(self):
+        csr, dev = self.csr, self.device
         self.plan, self.plan_reason = (None, "factorisation disabled")
-        fcl = cliques
+        fcl = self.cliques
         if not fcl and csr.n_in == csr.n and csr.nnz == csr.n * csr.n:
             fcl = [list(range(csr.n))]          # fully-connected: one clique (W = a I + c 11^T under MH)
-        if factor:
+        if self.factor:
             self.plan, self.plan_reason = build_clique_plan(csr, fcl)
-        if self.plan is not None:
-            p = self.plan
-            self.p_clique_ptr = torch.from_numpy(p.clique_ptr).to(dev)
-            self.p_member_row = torch.from_numpy(p.member_row).to(dev)
-            grp = p.member_group.copy()
-            if os.environ.get("NIIDMIX_GATEWAY_HINT", "1") != "0" and len(p.res_col):
-                # rows gathered as residual terms: loaded temporally by their own clique's item
-                grp[np.isin(p.member_row, p.res_col)] |= MEMBER_GATEWAY
-            self.p_member_group = torch.from_numpy(grp).to(dev)
-            self.p_coef = torch.from_numpy(np.ascontiguousarray(p.coef)).to(dev)
-            self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
-            self.p_res_col = torch.from_numpy(p.res_col).to(dev)
-            self.p_res_val = torch.from_numpy(p.res_val).to(dev)
-            self.p_res_member = torch.from_numpy(p.res_member).to(dev)
-        self.staged, self.staged_reason = build_staged_plan(csr, cliques) if cliques else \
-            build_staged_plan(csr, None)
-        if self.staged is not None:
-            sp = self.staged
-            self.s_blk_ptr = torch.from_numpy(sp.blk_ptr).to(dev)
-            self.s_blk_rows = torch.from_numpy(sp.blk_rows).to(dev)
-            self.s_src_ptr = torch.from_numpy(sp.src_ptr).to(dev)
-            self.s_src_rows = torch.from_numpy(sp.src_rows).to(dev)
-            self.s_scol = torch.from_numpy(sp.scol).to(dev)
-        # merged-order row tiles (exact mode's default kernel): only worth building when rows read
-        # many sources (avg degree >= 8); NIIDMIX_TILE_RT=8|16|32 picks the tile height (8 measured
-        # fastest: 5.9 ms vs 6.7 / 8.5 ms for 16 / 32 on the 1000-node d-cliques round)
+        if self.plan is None:
+            return
+        p = self.plan
+        self.p_clique_ptr = torch.from_numpy(p.clique_ptr).to(dev)
+        self.p_member_row = torch.from_numpy(p.member_row).to(dev)
+        grp = p.member_group.copy()
+        if os.environ.get("NIIDMIX_GATEWAY_HINT", "1") != "0" and len(p.res_col):
+            # rows gathered as residual terms: loaded temporally by their own clique's item
+            grp[np.isin(p.member_row, p.res_col)] |= MEMBER_GATEWAY
+        self.p_member_group = torch.from_numpy(grp).to(dev)
+        self.p_coef = torch.from_numpy(np.ascontiguousarray(p.coef)).to(dev)
+        self.p_res_ptr = torch.from_numpy(p.res_ptr).to(dev)
+        self.p_res_col = torch.from_numpy(p.res_col).to(dev)
+        self.p_res_val = torch.from_numpy(p.res_val).to(dev)
+        self.p_res_member = torch.from_numpy(p.res_member).to(dev)
+
+    def _build_tile(self):
+        # merged-order row tiles from global memory: only worth building when rows read many
+        # sources (avg degree >= 8); NIIDMIX_TILE_RT=8|16|32 picks the tile height
+        csr, dev = self.csr, self.device
         self.tile, self.tile_reason = (None, "average degree < 8")
         if csr.nnz >= 9 * max(csr.n, 1):
             rt = int(os.environ.get("NIIDMIX_TILE_RT", "8"))
-            self.tile, self.tile_reason = build_tile_plan(csr, cliques, rt)
-        if self.tile is not None:
-            tp = self.tile
-            self.t_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
-            self.t_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
-            self.t_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
-            self.t_pos_src = torch.from_numpy(tp.pos_src).to(dev)
-            self.t_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
-            self.t_pos_w = torch.from_numpy(tp.pos_w).to(dev)
-        # LDS-staged tiles (exact mode's default where they build: every clique's distinct source
+            self.tile, self.tile_reason = build_tile_plan(csr, self.cliques, rt)
+        if self.tile is None:
+            return
+        tp = self.tile
+        self.t_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+        self.t_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+        self.t_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+        self.t_pos_src = torch.from_numpy(tp.pos_src).to(dev)
+        self.t_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+        self.t_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+
+    def _build_tlds(self):
+        # LDS-staged tiles (exact mode's default where they build: every group's distinct source
         # rows fit the LDS stage); NIIDMIX_TILE_LDS_RT=8|16|32 picks the tile height
+        csr, dev = self.csr, self.device
         self.tlds, self.tlds_reason = (None, "average degree < 8")
         if csr.nnz >= 9 * max(csr.n, 1):
             rt = int(os.environ.get("NIIDMIX_TILE_LDS_RT", "16"))
-            grp = cliques
+            grp = self.cliques
             if not grp:
                 span = rt * LDS_MAX_WAVES.get(rt, 1)
                 grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
             self.tlds, self.tlds_reason = build_tile_lds_plan(csr, grp, rt)
-        if self.tlds is not None:
-            lp = self.tlds
-            tp = lp.tile
-            self.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
-            self.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
-            self.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
-            self.l_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
-            self.l_pos_slot = torch.from_numpy(lp.pos_slot).to(dev)
-            self.l_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
-            self.l_pos_w = torch.from_numpy(tp.pos_w).to(dev)
-            self.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
-            self.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
-            self.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
-        self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
-                      and self.n >= 64)
-        self.w_dense = torch.from_numpy(csr.dense()).to(dev) if self.dense else None
+        if self.tlds is None:
+            return
+        lp = self.tlds
+        tp = lp.tile
+        self.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
+        self.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
+        self.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
+        self.l_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
+        self.l_pos_slot = torch.from_numpy(lp.pos_slot).to(dev)
+        self.l_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
+        self.l_pos_w = torch.from_numpy(tp.pos_w).to(dev)
+        self.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
+        self.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
+        self.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
+
+    def _build_dense(self):
+        self.w_dense = torch.from_numpy(self.csr.dense()).to(self.device)
+
+    @property
+    def factored_safe(self):
+        """A clique plan exists and has no cancelling corrections (factor.CliquePlan.n_cancel)."""
+        return self.plan is not None and self.plan.n_cancel == 0
+
+    def _clique_args(self):
+        return (self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
+                self.p_res_ptr, self.p_res_col, self.p_res_val, self.p_res_member, self.row_ptr,
+                self.col, self.val)
 
     def mix_blocked(self, x, out, p, mode="fast", kernel=None):
         """One round on column-blocked slabs [K, rows, B] (niidmix.memory.empty_blocked): the
@@ -423,24 +453,25 @@ class Mixer:
         _req(self.plan.max_clique <= 1024, "blocked slabs: cliques of <= 1024 members (register "
              "tile, or the one-pass big-clique kernel); a bigger clique uses the two-pass kernel "
              "on [N, P] slabs")
-        mix_clique_blocked(x, self.p_clique_ptr, self.p_member_row, self.p_member_group,
-                           self.p_coef, self.p_res_ptr, self.p_res_col, self.p_res_val,
-                           self.p_res_member, out, int(p), self.plan.max_clique,
+        mix_clique_blocked(x, *self._clique_args(), out, int(p), self.plan.max_clique,
                            self.plan.max_clique_res)
         return out
 
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
-            # measured on the 1000-node d-cliques round (P = 2^20): merged-order row tiles of 8
-            # rows 5.9 ms, CSR gather 23.1 ms, LDS-staged 23.9 ms; the tile plan exists only for
-            # graphs with average degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
+            # measured on the 1000-node d-cliques round (P = 2^20): LDS-staged tiles 6.2 ms, global
+            # tiles 7.2 ms, CSR gather 23.1 ms; tile plans exist only for graphs with average
+            # degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
             if self.tlds is not None and (x is None or _lds_ok(x)) and (out is None or _lds_ok(out)):
                 return "tile-lds-exact"
             return "tile-exact" if self.tile is not None else "csr-exact"
-        if self.plan is not None and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
+        if self.factored_safe and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:
             return "dense"
+        if self.plan is not None and self.tlds is not None and (x is None or _lds_ok(x)) and \
+                (out is None or _lds_ok(out)):
+            return "tile-lds-fast"               # clique graph with removed edges
         return "csr-fast"
 
     def __call__(self, x, out=None, mode="fast", kernel=None):
@@ -452,11 +483,6 @@ class Mixer:
             mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT | hint)
         elif k == "csr-fast":
             mix_csr(x, self.row_ptr, self.col, self.val, out, FAST | hint)
-        elif k in ("staged-exact", "staged-fast"):
-            _req(self.staged is not None, f"no staged plan: {self.staged_reason}")
-            mix_staged(x, self.s_blk_ptr, self.s_blk_rows, self.s_src_ptr, self.s_src_rows,
-                       self.row_ptr, self.s_scol, self.val, out, self.staged.max_src,
-                       EXACT if k == "staged-exact" else FAST)
         elif k in ("tile-exact", "tile-fast"):
             _req(self.tile is not None, f"no tile plan: {self.tile_reason}")
             mix_tile(x, self.t_sub_ptr, self.t_sub_rows, self.t_sub_wself, self.t_pos_src,
@@ -471,14 +497,10 @@ class Mixer:
                          lp.max_tiles, EXACT if k == "tile-lds-exact" else FAST)
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
-            mix_clique(x, self.p_clique_ptr, self.p_member_row, self.p_member_group, self.p_coef,
-                       self.p_res_ptr, self.p_res_col, self.p_res_val, self.p_res_member, out,
-                       self.plan.max_clique,
+            mix_clique(x, *self._clique_args(), out, self.plan.max_clique,
                        self.plan.max_clique_res)
         elif k == "dense":
-            w = self.w_dense if self.w_dense is not None else \
-                torch.from_numpy(self.csr.dense()).to(x.device)
-            mix_dense(x, w, out)
+            mix_dense(x, self.w_dense, self.row_ptr, self.col, self.val, out)
         else:
             raise ValueError(f"unknown kernel {k!r}")
         return out

@@ -366,8 +366,10 @@ class StripedMixer:
         self.halo_rows = 0
         self.mode = mode
         self.mixer = ops.Mixer(csr=csr, cliques=cliques, device=self.device)
-        self.blocked = (mode == "fast" and self.mixer.plan is not None and
-                        self.mixer.plan.max_clique <= 256 and self.p_local % 4 == 0)
+        # column-blocked stripes whenever the factored kernels read them (register tile up to 256
+        # members, one-pass big-clique kernel up to 1024) and the plan has no cancelling terms
+        self.blocked = (mode == "fast" and self.mixer.factored_safe and
+                        self.mixer.plan.max_clique <= 1024 and self.p_local % 4 == 0)
 
     @classmethod
     def dcliques(cls, n_per_rank, clique_size, world, rank, interclique, device, p, seed=1337,

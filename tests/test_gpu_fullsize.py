@@ -1,0 +1,196 @@
+"""Parity of the shipped paths at the sizes they actually run (BASELINE.json configs[1..3]), through
+the same layouts and launch paths as bench.py and the drop-in:
+
+  * headline (configs[2]): the column-blocked VMM slab [1024, 1000, 1024] read directly by the clique
+    kernel, checked block by block against the oracle (no row-major round trip);
+  * fully-connected N=1000 (configs[3]): the blocked one-pass big-clique kernel at P = 2^20;
+  * ring N=100, P=62006 (configs[1]): the CSR kernel inside a hipGraph (bench.py's small-slab path),
+    fast and exact, two ping-pong rounds per graph;
+plus the non-finite guard on the blocked and two-pass layouts, and the consensus-distance event
+against the reference Logger's own numbers (tests/golden/consensus_*.npz).
+
+Columns of Θ' = Wᵀ Θ are independent (d_sgd.py:96-116 mixes every tensor element-wise), so any
+column window of the oracle is the full computation restricted to those columns.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+P_FULL = 1 << 20
+
+
+def _mixer(csr, cliques, dev):
+    from niidmix import ops
+    return ops.Mixer(csr=csr, cliques=cliques, device=dev)
+
+
+def _golden_csr(name):
+    from niidmix import ops
+    g = load_golden(name)
+    return g, ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+
+
+def _check_block(oracle_mod, csr, xw, yw, what):
+    ref = oracle_mod.mix_exact_c(xw, csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xw, csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(yw, ref, bound, rtol=RTOL)
+    assert ok, (what, worst)
+
+
+def _blocked_colsums(xb):
+    return torch.stack([xb[k].double().sum(0) for k in range(xb.shape[0])])
+
+
+def test_headline_blocked_vmm_slab_direct(gpu, oracle_mod):
+    """bench.py's headline round exactly as timed: VMM column-blocked slabs [1024, 1000, 1024],
+    mix_blocked (k_mix_clique<16,7,2,...>), checked on blocks 0, 511 and 1023 against the oracle
+    run on those blocks; every block's column sums are preserved (W doubly stochastic)."""
+    from niidmix import memory
+    g, csr = _golden_csr("dcliques1000_fc_p64")
+    m = _mixer(csr, g["cliques"], gpu)
+    xb = memory.empty_blocked(1000, P_FULL, gpu)
+    assert tuple(xb.shape) == (1024, 1000, 1024)
+    xb.normal_(generator=torch.Generator(device=gpu).manual_seed(0))
+    yb = memory.empty_blocked(1000, P_FULL, gpu)
+    m.mix_blocked(xb, yb, P_FULL)
+    torch.cuda.synchronize()
+    for k in (0, 511, 1023):
+        _check_block(oracle_mod, csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
+    assert torch.max(torch.abs(_blocked_colsums(xb) - _blocked_colsums(yb))).item() < 1e-3
+
+
+def test_fc1000_blocked_bigclique_fullsize(gpu, oracle_mod):
+    """bench.py --config fc1000 exactly as timed: MH fully-connected N=1000 (one clique of 1000,
+    W = a I + c 11^T), VMM column-blocked slabs, the one-pass register-resident big-clique kernel
+    (k_mix_bigclique_reg) at P = 2^20; blocks 0, 600 and 1023 against the oracle."""
+    from niidmix import memory
+    from niidmix.topology import mh_csr
+    n = 1000
+    csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
+    m = _mixer(csr, None, gpu)
+    assert m.kernel_for("fast") == "clique" and m.plan.max_clique == 1000
+    xb = memory.empty_blocked(n, P_FULL, gpu)
+    xb.normal_(generator=torch.Generator(device=gpu).manual_seed(1))
+    yb = memory.empty_blocked(n, P_FULL, gpu)
+    m.mix_blocked(xb, yb, P_FULL)
+    torch.cuda.synchronize()
+    for k in (0, 600, 1023):
+        _check_block(oracle_mod, csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
+    assert torch.max(torch.abs(_blocked_colsums(xb) - _blocked_colsums(yb))).item() < 1e-3
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_ring100_p62006_hipgraph(mode, gpu, oracle_mod):
+    """bench.py --config ring100 (P = 62006, rows 8-byte aligned: the float2 CSR path, 2 chunks per
+    wave for a low-degree graph) with the rounds captured in ONE hipGraph, as the bench times it:
+    two ping-pong rounds per replay, each checked against the oracle applied to that round's own
+    GPU input (bitwise in exact mode)."""
+    g, csr = _golden_csr("ring100_p257")
+    m = _mixer(csr, None, gpu)
+    p = 62006
+    kernel = m.kernel_for(mode)
+    assert kernel == ("csr-fast" if mode == "fast" else "csr-exact")
+    a = torch.randn(100, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(2))
+    b = torch.empty_like(a)
+    m(a, out=b, kernel=kernel, mode=mode)                   # warm-up outside the capture
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        m(a, out=b, kernel=kernel, mode=mode)
+        m(b, out=a, kernel=kernel, mode=mode)
+    for _ in range(2):
+        x0 = a.cpu().numpy()
+        graph.replay()
+        torch.cuda.synchronize()
+        y1, y2 = b.cpu().numpy(), a.cpu().numpy()
+        for xin, yout in ((x0, y1), (y1, y2)):
+            ref = oracle_mod.mix_exact_c(xin, csr.row_ptr, csr.col, csr.val)
+            if mode == "exact":
+                assert oracle_mod.bitwise_equal(yout, ref)
+            else:
+                bound = oracle_mod.condition_bound(xin, csr.row_ptr, csr.col, csr.val)
+                ok, worst = oracle_mod.check_tolerance(yout, ref, bound, rtol=RTOL)
+                assert ok, worst
+
+
+@pytest.mark.parametrize("name", ["nonfinite_dcliques300_fc_p64", "nonfinite_fc300_p36",
+                                  "nonfinite_dcliques200_fractal_rm5_p64"])
+def test_nonfinite_blocked_layout(name, gpu, oracle_mod):
+    """The non-finite guard on the device-resident layout: column-blocked slabs (block width 256)
+    through the clique / one-pass big-clique kernels give the reference's inf / NaN pattern."""
+    from niidmix import memory
+    g, csr = _golden_csr(name)
+    m = _mixer(csr, g.get("cliques"), gpu)
+    assert m.plan is not None, m.plan_reason
+    x = torch.from_numpy(g["x"]).to(gpu)
+    p = x.shape[1]
+    yb = memory.empty_blocked(m.n, p, gpu, 256)
+    m.mix_blocked(memory.to_blocked(x, 256), yb, p)
+    y = memory.from_blocked(yb, p).cpu().numpy()
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+    assert ok, worst
+
+
+@pytest.mark.parametrize("kernel_env", ["reg", "8x16", "16x1"])
+def test_nonfinite_bigclique_variants(kernel_env, gpu, oracle_mod, monkeypatch):
+    """Complete graph N=300 with ±inf / NaN / overflowing sums: the one-pass kernel and the two-pass
+    kernel (NIIDMIX_BIG=<waves>x<blocks per CU>) on row-major slabs, and the MFMA GEMM, all with the
+    reference's non-finite pattern."""
+    g, csr = _golden_csr("nonfinite_fc300_p36")
+    m = _mixer(csr, None, gpu)
+    monkeypatch.setenv("NIIDMIX_BIG", kernel_env)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    for kernel in ("clique", "dense"):
+        y = m(x, kernel=kernel).cpu().numpy()
+        ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+        assert ok, (kernel, worst)
+
+
+def test_auto_avoids_cancelling_plans(gpu):
+    """Removed clique edges: the factored plan exists but carries cancelling -c_g corrections, so
+    the auto choice takes the LDS tiles (fast) instead; explicit kernel='clique' is still served."""
+    g, csr = _golden_csr("dcliques200_fractal_rm5_p40")
+    m = _mixer(csr, g["cliques"], gpu)
+    assert m.plan is not None and m.plan.n_cancel > 0
+    assert m.kernel_for("fast") == "tile-lds-fast"
+    g, csr = _golden_csr("dcliques1000_fc_p64")
+    assert _mixer(csr, g["cliques"], gpu).kernel_for("fast") == "clique"
+
+
+@pytest.mark.parametrize("name", ["consensus_linear_n16", "consensus_n100_p4099"])
+def test_consensus_event_vs_reference_logger(name, gpu):
+    """niidmix.logger.consensus_distance_event against the event the reference's own
+    Logger.log_consensus_distance wrote for the same models (tests/golden/make_golden.py
+    --consensus).  The center is bit-identical (exact uniform average); distances are accumulated
+    in fp64 here and in fp32 per tensor by the reference (logger.py:42-48), hence rtol 1e-5 on
+    avg/max/min/norm and 1e-4 on std (a difference of nearly equal distances)."""
+    from niidmix import logger as nl
+    d = np.load(f"{GOLDEN}/{name}.npz")
+    shapes = [tuple(s) for s in json.loads(str(d["shapes_json"]))]
+    x = d["x"]
+    nodes = []
+    for r in range(x.shape[0]):
+        mdl = torch.nn.Module()
+        mdl.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(s)) for s in shapes])
+        off = 0
+        with torch.no_grad():
+            for q in mdl.parameters():
+                k = q.numel()
+                q.copy_(torch.from_numpy(x[r, off:off + k].copy()).view_as(q))
+                off += k
+        nodes.append({"rank": r, "model": mdl})
+    ev = nl.consensus_distance_event({"nodes": nodes, "step": 7})
+    ref = json.loads(str(d["event_json"]))
+    assert ev["type"] == ref["type"] and ev["step"] == ref["step"]
+    got, want = ev["distance_to_center"]["global"], ref["distance_to_center"]["global"]
+    for key in ("avg", "max", "min"):
+        np.testing.assert_allclose(got[key], want[key], rtol=1e-5, err_msg=key)
+    np.testing.assert_allclose(got["std"], want["std"], rtol=1e-4)
+    np.testing.assert_allclose(ev["center"]["norm"], ref["center"]["norm"], rtol=1e-5)

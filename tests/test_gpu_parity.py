@@ -27,12 +27,10 @@ def _mixer(g, dev, **kw):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact", "tile-exact"])
+@pytest.mark.parametrize("kernel", ["csr-exact", "tile-exact"])
 def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     m = _mixer(g, gpu)
-    if kernel == "staged-exact" and m.staged is None:
-        pytest.skip(f"no staged plan: {m.staged_reason}")
     if kernel == "tile-exact" and m.tile is None:
         m = _tile_mixer(g, gpu, 8)
     x = torch.from_numpy(g["x"]).to(gpu)
@@ -41,17 +39,17 @@ def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "staged-fast", "tile-fast"])
+@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "tile-fast"])
 def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
+    """Every fast kernel on every golden case, non-finite fixtures included: NaN where the
+    reference has NaN, the same inf where it has inf (the factored and GEMM kernels recompute
+    non-finite outputs from the CSR, include/niidmix.h), finite outputs within 1e-5 of the
+    condition bound."""
     g = load_golden(name)
-    if not np.all(np.isfinite(g["x"])):
-        pytest.skip("non-finite inputs: covered by the exact kernel")
     m = _mixer(g, gpu)
     p = g["x"].shape[1]
     if kernel == "clique" and (m.plan is None or p % 4):
         pytest.skip(f"no clique plan ({m.plan_reason}) or p % 4")
-    if kernel == "staged-fast" and m.staged is None:
-        pytest.skip(f"no staged plan ({m.staged_reason})")
     if kernel == "tile-fast" and m.tile is None:
         m = _tile_mixer(g, gpu, 16)
     x = torch.from_numpy(g["x"]).to(gpu)
@@ -197,7 +195,7 @@ def _windows(p, w=2048):
     return [(0, w), (p // 2 - w // 2, p // 2 + w // 2), (p - w, p)]
 
 
-@pytest.mark.parametrize("kernel", ["csr-exact", "staged-exact", "tile-exact"])
+@pytest.mark.parametrize("kernel", ["csr-exact", "tile-exact", "tile-lds-exact"])
 def test_full_size_exact_windows(kernel, gpu, oracle_mod):
     """BASELINE configs[2] at full size (N=1000 d-cliques, P=2^20): exact kernels are bit-identical
     to the oracle on sampled column windows (columns are independent)."""
