@@ -321,6 +321,16 @@ _LAZY = {
 }
 
 
+class _Scratch:
+    """Attribute sink for a Mixer plan builder: reads fall through to the Mixer."""
+
+    def __init__(self, owner):
+        self._owner = owner
+
+    def __getattr__(self, name):
+        return getattr(self._owner, name)
+
+
 class Mixer:
     """One topology's mixing operator on one device: Θ' = Wᵀ Θ for a [N, P] fp32 slab.
 
@@ -359,7 +369,13 @@ class Mixer:
         group = _LAZY.get(name)
         if group is None:
             raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
-        getattr(self, "_build_" + group)()
+        # build the group on a scratch object, then fill only what is not set yet: a caller (or a
+        # test) that installed its own plan keeps it
+        scratch = _Scratch(self)
+        getattr(type(self), "_build_" + group)(scratch)
+        for k, v in scratch.__dict__.items():
+            if k != "_owner" and k not in self.__dict__:
+                self.__dict__[k] = v
         return self.__dict__[name]
 
     def _build_clique(self):
