@@ -21,12 +21,19 @@ cpu_baseline (rank 0, N=1): the reference loop restated faithfully in torch CPU
 (oracle.reference_loop_average: per-node deepcopy / mul_(0) / add_(w*p), then update_models) timed
 on this host's cores for one full round of the same topology at the same P.
 
-Multi-GPU (N > 1): weak scaling over a d-cliques topology of 1000*N nodes (see --interclique).
---shard stripes (default): rank r mixes parameter columns [c0, c1) of EVERY node (P/N columns each,
-block-aligned; the round is independent per column), so per-rank bytes equal the N=1 round's and
-there is no data-path collective (niidmix.shard.StripedMixer).  --shard nodes: each rank owns 1000
-nodes (whole cliques) and the cross-shard edges' rows are exchanged over RCCL (xGMI) every round
-before the mixing kernel (niidmix.shard.ShardedMixer).
+Multi-GPU (N > 1), two problem sizes:
+  default (--config dcliques1000): WEAK scaling over a d-cliques topology of 1000*N nodes (see
+      --interclique), per-GPU bytes those of the N=1 headline round;
+  --config dcliques10000: BASELINE configs[4], the FIXED 10 000-node problem (100 cliques of 100)
+      split over N GPUs (STRONG scaling); rank 0 then also times the whole problem alone on its own
+      GPU (--single-ref, default on) and reports speedup_vs_1gpu.
+Two partitions:
+  --shard stripes (default): rank r mixes parameter columns [c0, c1) of EVERY node (P/N columns
+      each, block-aligned; the round is independent per column): no data-path collective
+      (niidmix.shard.StripedMixer);
+  --shard nodes: each rank owns whole cliques of nodes and the cross-shard edges' rows are
+      exchanged over RCCL (xGMI) every round, pipelined over column windows with the mixing kernel
+      (niidmix.shard.ShardedMixer); halo bytes per rank are reported.
 """
 import argparse
 import ctypes
@@ -95,6 +102,9 @@ def parse():
                          "or node shards with an RCCL halo exchange")
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
+    ap.add_argument("--single-ref", default="auto", choices=["auto", "on", "off"],
+                    help="multi-GPU fixed problem (--config dcliques10000): rank 0 also times the "
+                         "whole problem on its own GPU and reports the speed-up (auto: on)")
     return ap.parse_args()
 
 
@@ -225,6 +235,33 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
     return res
 
 
+def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
+    """One GPU, the whole d-cliques problem of n nodes: the headline kernel on column-blocked VMM
+    slabs (2 x n*p*4 bytes), mean of `steps` rounds after `warmup`."""
+    from niidmix import memory, ops
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(n, 100, interclique, 1337)
+    m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+    xa = memory.empty_blocked(n, p, dev)
+    xa.normal_(generator=torch.Generator(device=dev).manual_seed(7))
+    xb = memory.empty_blocked(n, p, dev)
+    for _ in range(warmup):
+        m.mix_blocked(xa, xb, p)
+        xa, xb = xb, xa
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    s.record()
+    for _ in range(steps):
+        m.mix_blocked(xa, xb, p)
+        xa, xb = xb, xa
+    e.record()
+    torch.cuda.synchronize(dev)
+    ms = s.elapsed_time(e) / steps
+    del xa, xb
+    torch.cuda.empty_cache()
+    return ms
+
+
 def load_traffic(path, key):
     try:
         with open(path) as f:
@@ -347,6 +384,10 @@ def main():
     from niidmix import memory, ops
     if args.workload != "mix" and world > 1:
         raise SystemExit("--workload grad-clique is single-GPU")
+    fixed = world > 1 and args.config == "dcliques10000"       # BASELINE configs[4]: strong scaling
+    if world > 1 and args.config not in ("dcliques1000", "dcliques10000"):
+        raise SystemExit("multi-GPU: --config dcliques1000 (weak, 1000 nodes per GPU) or dcliques10000")
+    n_multi = 10000 if fixed else args.nodes_per_gpu * world
     if world == 1:
         csr, cliques, p_default, desc = single_gpu_topology(args.config)
         p = args.p or p_default
@@ -389,7 +430,7 @@ def main():
     elif args.shard == "stripes":
         from niidmix.shard import StripedMixer
         p = args.p or (1 << 20)
-        mixer = StripedMixer.dcliques(n_per_rank=args.nodes_per_gpu, clique_size=100, world=world,
+        mixer = StripedMixer.dcliques(n_total=n_multi, clique_size=100, world=world,
                                       rank=rank, interclique=args.interclique, device=dev, p=p,
                                       mode="exact" if args.kernel.endswith("exact") else "fast")
         n_local, n_total = mixer.n_local, mixer.n_total
@@ -406,14 +447,14 @@ def main():
     else:
         from niidmix.shard import ShardedMixer
         p = args.p or (1 << 20)
-        mixer = ShardedMixer.dcliques(n_per_rank=args.nodes_per_gpu, clique_size=100, world=world, rank=rank,
+        mixer = ShardedMixer.dcliques(n_total=n_multi, clique_size=100, world=world, rank=rank,
                                       interclique=args.interclique, device=dev, p=p,
                                       windows=args.windows)
         n_local, n_total = mixer.n_local, mixer.n_total
         halo = mixer.halo_rows
         cols_local = p
         desc = (f"d-cliques N={n_total} ({n_total // 100} cliques x 100, {args.interclique} "
-                f"interclique, MH), {args.nodes_per_gpu} nodes per GPU; halo rows over RCCL")
+                f"interclique, MH), {n_total // world} nodes per GPU on average; halo rows over RCCL")
         parallelism = (f"{world} clique-aligned node shards, RCCL (xGMI) halo exchange pipelined "
                        f"over {mixer.k} column windows")
         csr = None
@@ -489,6 +530,18 @@ def main():
         region_s, launch_ms = tt.tolist()
     step_s = region_s / args.steps
     value = n_total * p * 4 / step_s / 1e9
+    slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}]"
+                   if xa.dim() == 3 and (blocked or args.shard == "stripes") else
+                   "window-blocked [K, rows_in, w]" if xa.dim() == 3 else "row-major [N, P]")
+    single = None
+    if fixed and args.single_ref != "off":
+        # the same fixed problem on ONE GPU (rank 0's), same kernel and layout: the N=1 point of
+        # this strong-scaling line, measured in the same run; the other ranks wait
+        del xa, xb
+        torch.cuda.empty_cache()
+        if rank == 0:
+            single = single_gpu_round_ms(n_total, p, args.interclique, dev, args.steps, args.warmup)
+        dist.barrier()
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
     if rank == 0:
@@ -522,7 +575,7 @@ def main():
         out = {
             "metric": METRIC if args.workload == "mix" else GRAD_METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "strong" if fixed else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded N(0,1) [N,P] fp32 slab resident in HBM; topology from the "
                     "reference's generators)",
             "config": {"workload": desc, "n_nodes": n_total, "p": p, "kernel": kernel,
@@ -532,11 +585,7 @@ def main():
                        "slab_memory": ("hipMalloc" if args.hipmalloc_slabs or
                                        (world > 1 and args.shard == "nodes")
                                        else "VMM 2 MiB chunks (niidmix_hbm_alloc)"),
-                       "slab_layout": (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, "
-                                       f"{xa.shape[2]}]" if xa.dim() == 3 and
-                                       (blocked or args.shard == "stripes") else
-                                       "window-blocked [K, rows_in, w]" if xa.dim() == 3 else
-                                       "row-major [N, P]"),
+                       "slab_layout": slab_layout,
                        "stream_copy_GBs": round(copy_gbs, 1),
                        "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
                                                if roof["unit"] == "GB/s" else None)},
@@ -545,6 +594,12 @@ def main():
         }
         if e2e is not None:
             out["e2e"] = e2e
+        if world > 1 and args.shard == "nodes":
+            out["config"]["halo_GB_recv_rank0"] = round(mixer.halo_bytes / 1e9, 3)
+            out["config"]["halo_GB_send_rank0"] = round(mixer.send_bytes / 1e9, 3)
+        if single is not None:
+            out["config"]["single_gpu_ms"] = round(single, 4)
+            out["config"]["speedup_vs_1gpu"] = round(single / (step_s * 1e3), 3)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

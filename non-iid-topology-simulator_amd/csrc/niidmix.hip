@@ -473,49 +473,46 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xr[q][e], v[r][e]);
             }
     }
-    // overflow: entries past the RQ held per wave, and clique entries past the RW fetched
-    // lane-parallel (scalar loads, one gather at a time)
-    // (OVB gathers in flight per batch; the registers of xr[] are free again here)
-    while (mine) {
-        float xo[OVB][V];
-        int jo[OVB];
+    // overflow: entries past the RQ held per wave (OVB gathers in flight per batch; the registers
+    // of xr[] are free again here), then the clique's entries past the first RW, 64 descriptors at
+    // a time fetched lane-parallel into the same descriptor registers and gathered in OVB batches
+    // (a 10 000-node d-cliques clique has 99 gateway entries; N=8 column stripes 79)
+    for (int32_t cb = d.cr0 + nl;;) {
+        while (mine) {
+            float xo[OVB][V];
+            int jo[OVB];
 #pragma unroll
-        for (int b = 0; b < OVB; ++b) {
-            jo[b] = mine ? __builtin_ctzll(mine) : -1;
-            mine &= mine - 1;
-            const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jo[b] >= 0 ? jo[b] : 0);
+            for (int b = 0; b < OVB; ++b) {
+                jo[b] = mine ? __builtin_ctzll(mine) : -1;
+                mine &= mine - 1;
+                const int64_t row = __builtin_amdgcn_readlane(d.rsrc, jo[b] >= 0 ? jo[b] : 0);
 #pragma unroll
-            for (int e = 0; e < V; ++e) xo[b][e] = 0.f;
-            if (act && jo[b] >= 0) ldv<V>(xc + row * ld_x + lo, xo[b]);
-        }
-#pragma unroll
-        for (int b = 0; b < OVB; ++b) {
-            if (jo[b] < 0) break;                                       // wave-uniform
-            const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), jo[b]));
-            const int slot = __builtin_amdgcn_readlane(d.rk, jo[b]) / WAVES;
-#pragma unroll
-            for (int r = 0; r < RPW; ++r)
-                if (slot == r) {
-#pragma unroll
-                    for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[b][e], v[r][e]);
-                }
-        }
-    }
-    for (int32_t q = d.cr0 + nl; q < d.cr0 + ncr; ++q) {
-        const int k = res_member[q];
-        if (k % WAVES != wave) continue;                                // wave-uniform
-        float xo[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) xo[e] = 0.f;
-        if (act) ldv<V>(xc + (int64_t)res_col[q] * ld_x + lo, xo);
-        const float w = res_val[q];
-        const int slot = k / WAVES;
-#pragma unroll
-        for (int r = 0; r < RPW; ++r)
-            if (slot == r) {
-#pragma unroll
-                for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[e], v[r][e]);
+                for (int e = 0; e < V; ++e) xo[b][e] = 0.f;
+                if (act && jo[b] >= 0) ldv<V>(xc + row * ld_x + lo, xo[b]);
             }
+#pragma unroll
+            for (int b = 0; b < OVB; ++b) {
+                if (jo[b] < 0) break;                                   // wave-uniform
+                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.rw), jo[b]));
+                const int slot = __builtin_amdgcn_readlane(d.rk, jo[b]) / WAVES;
+#pragma unroll
+                for (int r = 0; r < RPW; ++r)
+                    if (slot == r) {
+#pragma unroll
+                        for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(w, xo[b][e], v[r][e]);
+                    }
+            }
+        }
+        if (cb >= d.cr0 + ncr) break;                                   // wave-uniform
+        const int32_t cnt = d.cr0 + ncr - cb < 64 ? d.cr0 + ncr - cb : 64;
+        d.rsrc = 0; d.rk = -1; d.rw = 0.f;
+        if (lane < cnt) {
+            d.rsrc = res_col[cb + lane];
+            d.rk = res_member[cb + lane];
+            d.rw = res_val[cb + lane];
+        }
+        mine = __ballot(lane < cnt && d.rk % WAVES == wave);
+        cb += 64;
     }
     // 4. group sums across waves through LDS (waves 0..G-1 each reduce one group)
     if (!NO_RED) __syncthreads();

@@ -142,12 +142,13 @@ def _fused_ok(params):
 
 
 class _FusedEngine:
-    """Parameter slab + gradient slab + GradMean + Mixer + FusedRoundRunner."""
+    """Parameter slab + gradient slab + GradMean + Mixer + FusedRoundRunner (one per GPU stripe
+    when several GPUs are visible, niidmix.slab.MultiDeviceRound)."""
 
-    def __init__(self, nodes, topology, params, device):
+    def __init__(self, nodes, topology, params, devices):
         from .gradient import GradMean, build_grad_plan
         from .ops import Mixer
-        from .slab import FusedRoundRunner, NodeSlab
+        from .slab import FusedRoundRunner, MultiDeviceRound, NodeSlab
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
         self.key = _grad_key(params) + (float(params["algorithm"]["learning-rate"]),)
@@ -158,11 +159,14 @@ class _FusedEngine:
         csr = to_csr(topology)
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
-        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=device)
-        self.runner = FusedRoundRunner(GradMean(self.plan, device), self.plan.stepped,
-                                       params["algorithm"]["learning-rate"], self.mixer,
-                                       self.slab.n, self.slab.p, device,
-                                       window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
+        lr = params["algorithm"]["learning-rate"]
+
+        def make(dev, n, cols):
+            mixer = self.mixer if dev == devices[0] else self.mixer.to(dev)
+            return FusedRoundRunner(GradMean(self.plan, dev), self.plan.stepped, lr, mixer, n,
+                                    cols, dev, window=_window())
+        self.runner = MultiDeviceRound(make, self.slab.n, self.slab.p, devices)
 
     def valid_for(self, nodes, topology, params):
         models = [n["model"] for n in nodes]
@@ -181,8 +185,7 @@ def fused_round(nodes, topology, params):
     key = id(nodes)
     eng = _fused_engines.get(key)
     if eng is None or not eng.valid_for(nodes, topology, params):
-        dev = torch.device("cuda", torch.cuda.current_device())
-        eng = _FusedEngine(nodes, topology, params, dev)
+        eng = _FusedEngine(nodes, topology, params, _devices(nodes))
         _fused_engines.clear()
         _fused_engines[key] = eng
     logging.info("  fused gradient %s + SGD step + mixing (GPU, %s)", eng.plan.kind, _mode(params))
@@ -194,25 +197,38 @@ def fused_round(nodes, topology, params):
 
 # ------------------------------------------------------------------------------------------------
 # the GPU mixing step
-class _Engine:
-    """NodeSlab + Mixer + SlabMixer for one (node list, topology) pair."""
+def _window():
+    return int(os.environ.get("NIIDMIX_WINDOW", 1 << 15))
 
-    def __init__(self, nodes, topology, device):
+
+class _Engine:
+    """NodeSlab + Mixer + SlabMixer for one (node list, topology) pair.  With several GPUs
+    visible (niidmix.slab.mixing_devices) the round is split into parameter-column stripes, one per
+    GPU, each streamed over its own PCIe link (niidmix.slab.MultiDeviceRound); bitwise the same."""
+
+    def __init__(self, nodes, topology, devices):
         from .ops import Mixer
-        from .slab import NodeSlab, SlabMixer
+        from .slab import MultiDeviceRound, NodeSlab, SlabMixer
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
         self.slab = NodeSlab([n["model"] for n in nodes])
         csr = to_csr(topology)
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
-        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=device)
-        self.runner = SlabMixer(self.mixer, self.slab.n, self.slab.p, device,
-                                window=int(os.environ.get("NIIDMIX_WINDOW", 1 << 15)))
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
+        self.runner = MultiDeviceRound(
+            lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
+                                           n, cols, dev, window=_window()),
+            self.slab.n, self.slab.p, devices)
+
+    def mix(self, mode, timing):
+        self.runner.run(self.slab.host, mode=mode, timing=timing)
+        return self.runner.last_timing
 
     def valid_for(self, nodes, topology):
         return (topology is self.topology and id(topology.get("weights")) == self.weights_id
                 and self.slab.owns([n["model"] for n in nodes]))
+
 
 
 _engines = {}
@@ -233,13 +249,25 @@ def average(nodes, topology, params):
     key = id(nodes)
     eng = _engines.get(key)
     if eng is None or not eng.valid_for(nodes, topology):
-        dev = torch.device("cuda", torch.cuda.current_device())
-        eng = _Engine(nodes, topology, dev)
+        eng = _Engine(nodes, topology, _devices(nodes))
         _engines.clear()
         _engines[key] = eng
-    eng.runner.mix(eng.slab.host, mode=_mode(params), timing=logging.getLogger().isEnabledFor(logging.INFO))
-    if eng.runner.last_timing:
-        logging.info("  mixing round: %s", eng.runner.last_timing)
+    t = eng.mix(_mode(params), logging.getLogger().isEnabledFor(logging.INFO))
+    if t:
+        logging.info("  mixing round: %s", t)
+
+
+def _devices(nodes):
+    """GPUs the host-resident round uses (niidmix.slab.mixing_devices; NIIDMIX_DEVICES selects),
+    the current device first."""
+    from .slab import mixing_devices
+    p = sum(q.numel() for q in nodes[0]["model"].parameters())
+    cur = torch.cuda.current_device()
+    devs = mixing_devices(p)
+    if not os.environ.get("NIIDMIX_DEVICES"):
+        order = [cur] + [d.index for d in devs if d.index != cur]
+        devs = [torch.device("cuda", i) for i in order[:len(devs)]]
+    return devs
 
 
 # ------------------------------------------------------------------------------------------------

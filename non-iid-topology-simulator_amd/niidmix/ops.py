@@ -362,8 +362,22 @@ class Mixer:
         self.row_ptr = torch.from_numpy(csr.row_ptr).to(dev)
         self.col = torch.from_numpy(csr.col).to(dev)
         self.val = torch.from_numpy(csr.val).to(dev)
+        self.dense_threshold = dense_threshold
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
+        self._host = {}           # host-side plans, shared with the Mixers .to() makes
+
+    def to(self, device):
+        """The same operator on another device, sharing the host-side plans (built once)."""
+        m = Mixer(csr=self.csr, cliques=self.cliques, device=device,
+                  dense_threshold=self.dense_threshold, factor=self.factor)
+        m._host = self._host
+        return m
+
+    def _hosted(self, key, build):
+        if key not in self._host:
+            self._host[key] = build()
+        return self._host[key]
 
     def __getattr__(self, name):
         group = _LAZY.get(name)
@@ -385,7 +399,7 @@ class Mixer:
         if not fcl and csr.n_in == csr.n and csr.nnz == csr.n * csr.n:
             fcl = [list(range(csr.n))]          # fully-connected: one clique (W = a I + c 11^T under MH)
         if self.factor:
-            self.plan, self.plan_reason = build_clique_plan(csr, fcl)
+            self.plan, self.plan_reason = self._hosted("clique", lambda: build_clique_plan(csr, fcl))
         if self.plan is None:
             return
         p = self.plan
@@ -409,7 +423,8 @@ class Mixer:
         self.tile, self.tile_reason = (None, "average degree < 8")
         if csr.nnz >= 9 * max(csr.n, 1):
             rt = int(os.environ.get("NIIDMIX_TILE_RT", "8"))
-            self.tile, self.tile_reason = build_tile_plan(csr, self.cliques, rt)
+            self.tile, self.tile_reason = self._hosted(
+                ("tile", rt), lambda: build_tile_plan(csr, self.cliques, rt))
         if self.tile is None:
             return
         tp = self.tile
@@ -431,7 +446,8 @@ class Mixer:
             if not grp:
                 span = rt * LDS_MAX_WAVES.get(rt, 1)
                 grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
-            self.tlds, self.tlds_reason = build_tile_lds_plan(csr, grp, rt)
+            self.tlds, self.tlds_reason = self._hosted(
+                ("tlds", rt), lambda: build_tile_lds_plan(csr, grp, rt))
         if self.tlds is None:
             return
         lp = self.tlds

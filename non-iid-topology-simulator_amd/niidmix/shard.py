@@ -291,11 +291,21 @@ class ShardedMixer:
             dist.barrier(group=group)   # first collective: every rank joins before any P2P
 
     @classmethod
-    def dcliques(cls, n_per_rank, clique_size, world, rank, interclique, device, p, seed=1337,
+    def dcliques(cls, n_total, clique_size, world, rank, interclique, device, p, seed=1337,
                  windows=8, group=None):
         from .generate import dcliques_csr
-        csr, cliques = dcliques_csr(n_per_rank * world, clique_size, interclique, seed)
+        csr, cliques = dcliques_csr(n_total, clique_size, interclique, seed)
         return cls(csr, cliques, world, rank, device, p, windows=windows, group=group)
+
+    @property
+    def halo_bytes(self):
+        """Bytes this rank receives per round (its halo rows x p fp32 columns)."""
+        return self.halo_rows * self.p * 4
+
+    @property
+    def send_bytes(self):
+        """Bytes this rank sends per round (every row some peer reads, once per reading peer)."""
+        return sum(len(v) for v in self.shard.send.values()) * self.p * 4
 
     def empty(self):
         return torch.empty((self.k, self.rows_in, self.w), dtype=torch.float32, device=self.device)
@@ -372,10 +382,10 @@ class StripedMixer:
                         self.mixer.plan.max_clique <= 1024 and self.p_local % 4 == 0)
 
     @classmethod
-    def dcliques(cls, n_per_rank, clique_size, world, rank, interclique, device, p, seed=1337,
+    def dcliques(cls, n_total, clique_size, world, rank, interclique, device, p, seed=1337,
                  mode="fast"):
         from .generate import dcliques_csr
-        csr, cliques = dcliques_csr(n_per_rank * world, clique_size, interclique, seed)
+        csr, cliques = dcliques_csr(n_total, clique_size, interclique, seed)
         return cls(csr, cliques, world, rank, device, p, mode=mode)
 
     def empty(self):

@@ -15,6 +15,7 @@ window k's inputs are on the device before its outputs are written back, and win
 columns.
 """
 import ctypes
+import os
 import time
 
 import torch
@@ -110,6 +111,15 @@ class SlabMixer:
 
     def mix(self, host, mode="exact", kernel=None, timing=False):
         """host: pinned fp32 [N, P] (may be any row-major slab with stride(1) == 1)."""
+        t0 = time.perf_counter()
+        self.launch(host, mode=mode, kernel=kernel, timing=timing)
+        self.wait()
+        if timing:
+            self.last_timing["round_s"] = time.perf_counter() - t0
+        return host
+
+    def launch(self, host, mode="exact", kernel=None, timing=False):
+        """Enqueue the round (H2D / mix / D2H of every window) without waiting for it."""
         n, p, w = self.n, self.p, self.window
         assert host.shape == (n, p) and host.dtype == torch.float32 and host.stride(1) == 1
         ld_h = host.stride(0) * 4
@@ -119,10 +129,11 @@ class SlabMixer:
         ev_mix = [torch.cuda.Event() for _ in range(nwin)]
         ev_out = [torch.cuda.Event() for _ in range(nwin)]
         t_ev = None
+        self._timing = timing
         if timing:
             t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            t0 = time.perf_counter()
             t_ev[0].record(self.s_h2d)
+        self._t_ev, self._nwin = t_ev, nwin
         for k in range(nwin):
             c0 = k * w
             cw = min(w, p - c0)
@@ -147,25 +158,29 @@ class SlabMixer:
                 ev_out[k].record(self.s_d2h)
         if timing:
             t_ev[1].record(self.s_d2h)
+
+    def wait(self):
         self.s_d2h.synchronize()
-        if timing:
-            self.last_timing = {"round_s": time.perf_counter() - t0,
-                                "gpu_span_s": t_ev[0].elapsed_time(t_ev[1]) / 1e3,
-                                "windows": nwin, "window_cols": w}
-        return host
+        if self._timing:
+            t_ev = self._t_ev
+            self.last_timing = {"gpu_span_s": t_ev[0].elapsed_time(t_ev[1]) / 1e3,
+                                "windows": self._nwin, "window_cols": self.window}
 
 
 class FusedRoundRunner:
     """One drop-in round with gradient averaging, fused on the device:
     per column window, H2D of the parameter AND gradient slabs, then on the device
         gradient mean (GradMean)  ->  SGD step on the stepped rows  ->  mixing (Mixer)
-    and D2H of the mixed parameters only.  The reference's equivalent is d_sgd.gradient (CPU mean
-    + optimizer.step on every stepped node) followed by d_sgd.average; per window the arithmetic is
-    the same, bit for bit, and columns are independent, so windows pipeline as in SlabMixer.
-    The host gradients keep the nodes' own gradients (the reference leaves the averaged ones
-    there until the next zero_grad; nothing reads them in between)."""
+    and D2H of the mixed parameters and of the averaged gradients.  The reference's equivalent is
+    d_sgd.gradient (CPU mean + optimizer.step on every stepped node) followed by d_sgd.average; per
+    window the arithmetic is the same, bit for bit, and columns are independent, so windows
+    pipeline as in SlabMixer.  The averaged gradients are written back to the host gradient slab,
+    where the reference leaves them until the next zero_grad (update_gradients, d_sgd.py:37-45);
+    grad_writeback=False (NIIDMIX_GRAD_WRITEBACK=0) skips that D2H for callers that never read
+    .grad between rounds (the round is then H2D-bound: 8.4 GB per headline round)."""
 
-    def __init__(self, grad_op, step_rows, lr, mixer, n, p, device, window=1 << 15):
+    def __init__(self, grad_op, step_rows, lr, mixer, n, p, device, window=1 << 15,
+                 grad_writeback=None):
         self.grad_op = grad_op
         self.mixer = mixer
         self.n, self.p = n, p
@@ -178,13 +193,27 @@ class FusedRoundRunner:
         self.dp = [mk(), mk()]
         self.dg = [mk(), mk()]
         self.dy = [mk(), mk()]
-        self.dm = mk()
+        self.dm = [mk(), mk()]
+        if grad_writeback is None:
+            grad_writeback = os.environ.get("NIIDMIX_GRAD_WRITEBACK", "1") != "0"
+        self.grad_writeback = grad_writeback
         self.s_h2d = torch.cuda.Stream(self.device)
         self.s_mix = torch.cuda.Stream(self.device)
         self.s_d2h = torch.cuda.Stream(self.device)
         self.last_timing = None
 
     def run(self, host_params, host_grads, mode="exact", timing=False):
+        t0 = time.perf_counter()
+        self.launch(host_params, host_grads, mode=mode)
+        self.wait()
+        if timing:
+            self.last_timing = {"round_s": time.perf_counter() - t0,
+                                "windows": (self.p + self.window - 1) // self.window,
+                                "window_cols": self.window}
+        return host_params
+
+    def launch(self, host_params, host_grads, mode="exact"):
+        """Enqueue the fused round of every window without waiting for it."""
         from . import ops
         n, p, w = self.n, self.p, self.window
         for h in (host_params, host_grads):
@@ -195,7 +224,6 @@ class FusedRoundRunner:
         ev_in = [torch.cuda.Event() for _ in range(nwin)]
         ev_mix = [torch.cuda.Event() for _ in range(nwin)]
         ev_out = [torch.cuda.Event() for _ in range(nwin)]
-        t0 = time.perf_counter()
         for k in range(nwin):
             c0 = k * w
             cw = min(w, p - c0)
@@ -210,7 +238,7 @@ class FusedRoundRunner:
                 self.s_mix.wait_event(ev_in[k])
                 if k >= 2:
                     self.s_mix.wait_event(ev_out[k - 2])
-                xp, xg, gm = self.dp[buf][:, :cw], self.dg[buf][:, :cw], self.dm[:, :cw]
+                xp, xg, gm = self.dp[buf][:, :cw], self.dg[buf][:, :cw], self.dm[buf][:, :cw]
                 self.grad_op(xg, out=gm)
                 if self.rows.numel():
                     ops.sgd_step_rows(xp, gm, self.rows, self.neg_lr)
@@ -219,9 +247,68 @@ class FusedRoundRunner:
             with torch.cuda.stream(self.s_d2h):
                 self.s_d2h.wait_event(ev_mix[k])
                 _copy2d(bp + c0 * 4, ld_p, self.dy[buf].data_ptr(), w * 4, cw * 4, n, 1, self.s_d2h)
+                if self.grad_writeback:
+                    _copy2d(bg + c0 * 4, ld_g, self.dm[buf].data_ptr(), w * 4, cw * 4, n, 1,
+                            self.s_d2h)
                 ev_out[k].record(self.s_d2h)
+
+    def wait(self):
         self.s_d2h.synchronize()
+
+
+# ------------------------------------------------------------------------------------------------
+# several GPUs in ONE process (the simulator is one process, run.py:136)
+MIN_STRIPE_COLS = 1 << 16
+
+
+def mixing_devices(p, devices=None):
+    """The devices a host-resident round of P columns is spread over: NIIDMIX_DEVICES
+    ("0,1,2,3"), else every visible GPU, but at most one per MIN_STRIPE_COLS columns (a LeNet-size
+    model stays on one GPU; a 1M-parameter model uses up to 16)."""
+    if devices is None:
+        env = os.environ.get("NIIDMIX_DEVICES")
+        if env:
+            devices = [torch.device("cuda", int(i)) for i in env.split(",") if i.strip()]
+        else:
+            devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    devices = [torch.device(d) for d in devices]
+    k = max(1, min(len(devices), -(-p // MIN_STRIPE_COLS)))
+    return devices[:k]
+
+
+class MultiDeviceRound:
+    """One host-resident round spread over several GPUs of this process by parameter-column
+    stripes (niidmix.shard.column_stripe: the round is independent per column, d_sgd.py:96-116
+    mixes every tensor element-wise), with no exchange between the GPUs: each device runs its own
+    window pipeline (its own streams, buffers and PCIe link) on its stripe of the pinned slab(s),
+    all devices enqueued before any is waited for.
+
+      make(device, n, cols) -> a runner with launch(*host_stripes, **kw) / wait()
+                               (SlabMixer, FusedRoundRunner)
+    Results are bitwise those of one device: same kernels, same per-column arithmetic."""
+
+    def __init__(self, make, n, p, devices, align=1024):
+        from .shard import column_stripe
+        self.n, self.p = n, p
+        self.devices = [torch.device(d) for d in devices]
+        world = len(self.devices)
+        self.stripes = [column_stripe(p, world, r, align) for r in range(world)]
+        self.runners = []
+        for dev, (c0, c1) in zip(self.devices, self.stripes):
+            self.runners.append(make(dev, n, c1 - c0) if c1 > c0 else None)
+        self.last_timing = None
+
+    def run(self, *hosts, timing=False, **kw):
+        t0 = time.perf_counter()
+        for runner, (c0, c1) in zip(self.runners, self.stripes):
+            if runner is not None:
+                with torch.cuda.device(runner.device):
+                    runner.launch(*[h[:, c0:c1] for h in hosts], **kw)
+        for runner in self.runners:
+            if runner is not None:
+                runner.wait()
         if timing:
-            self.last_timing = {"round_s": time.perf_counter() - t0, "windows": nwin,
-                                "window_cols": w}
-        return host_params
+            self.last_timing = {"round_s": time.perf_counter() - t0,
+                                "devices": [str(d) for d in self.devices],
+                                "stripes": self.stripes}
+        return hosts[0]

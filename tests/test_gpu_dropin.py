@@ -221,13 +221,16 @@ def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
         finally:
             d_sgd.gradient, d_sgd.average = orig_g, orig_a
-        return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
+        return [(torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone(),
+                 torch.cat([q.grad.detach().reshape(-1) for q in n["model"].parameters()]).clone())
                 for n in nodes]
 
     fused, unfused, ref = run("fused"), run("unfused"), run("oracle")
     for u, v, r in zip(fused, unfused, ref):
-        assert torch.equal(v, r)
-        assert torch.equal(u, r)
+        assert torch.equal(v[0], r[0]) and torch.equal(v[1], r[1])
+        assert torch.equal(u[0], r[0])
+        # the fused round writes the averaged gradients back where the reference leaves them
+        assert torch.equal(u[1], r[1])
 
 
 def test_sgd_step_rows_matches_torch_cpu_sgd(gpu):
@@ -272,3 +275,58 @@ def test_consensus_distance_event(gpu, tmp_path):
     import json
     line = json.loads(open(L.global_events).read().strip())
     assert line["step"] == 5 and "distance_to_center" in line
+
+
+@pytest.mark.parametrize("stripes", [2, 3])
+def test_multi_device_round_bitwise(stripes, gpu, oracle_mod):
+    """The single-process multi-GPU drop-in round (niidmix.slab.MultiDeviceRound: one column stripe
+    per device, each with its own streams and window pipeline, no exchange) with every stripe
+    mapped to the one GPU of this box: bitwise the single-device round, exact and fast mode, and
+    the exact round bitwise the reference fixture (d-cliques N=300)."""
+    from niidmix import ops
+    from niidmix.slab import MultiDeviceRound, SlabMixer
+    g = load_golden("dcliques300_fc_p37")
+    csr = ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    m = ops.Mixer(csr=csr, cliques=g["cliques"], device=gpu)
+    n, p = 300, 5000
+    gen = torch.Generator().manual_seed(stripes)
+    x = torch.randn(n, p, generator=gen)
+    for mode in ("exact", "fast"):
+        h1 = x.clone().pin_memory()
+        SlabMixer(m, n, p, gpu, window=1024).mix(h1, mode=mode)
+        hk = x.clone().pin_memory()
+        mr = MultiDeviceRound(lambda dev, nn, cols: SlabMixer(m.to(dev), nn, cols, dev, window=1024),
+                              n, p, [gpu] * stripes, align=256)
+        assert len([r for r in mr.runners if r is not None]) == stripes
+        mr.run(hk, mode=mode)
+        assert torch.equal(hk, h1), mode
+    h = torch.from_numpy(g["x"]).clone().pin_memory()
+    mr = MultiDeviceRound(lambda dev, nn, cols: SlabMixer(m.to(dev), nn, cols, dev), 300, 37,
+                          [gpu] * stripes, align=16)
+    mr.run(h, mode="exact")
+    assert oracle_mod.bitwise_equal(h.numpy(), g["y"])
+
+
+def test_multi_device_fused_round_bitwise(gpu):
+    """The fused gradient + step + mixing round over 3 stripes on one GPU equals one device's."""
+    from niidmix import ops
+    from niidmix.gradient import GradMean, build_grad_plan
+    from niidmix.slab import FusedRoundRunner, MultiDeviceRound
+    g = load_golden("dcliques300_fc_p37")
+    csr = ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    m = ops.Mixer(csr=csr, cliques=g["cliques"], device=gpu)
+    plan = build_grad_plan(300, {"cliques": g["cliques"], "edges": csr.edges()},
+                           {"algorithm": {"clique-gradient": True}})
+    n, p = 300, 4100
+    gen = torch.Generator().manual_seed(9)
+    xp, xg = torch.randn(n, p, generator=gen), torch.randn(n, p, generator=gen)
+
+    def make(dev, nn, cols):
+        return FusedRoundRunner(GradMean(plan, dev), plan.stepped, 0.1, m.to(dev), nn, cols, dev,
+                                window=1024)
+    hp1, hg1 = xp.clone().pin_memory(), xg.clone().pin_memory()
+    make(gpu, n, p).run(hp1, hg1, mode="exact")
+    hp3, hg3 = xp.clone().pin_memory(), xg.clone().pin_memory()
+    MultiDeviceRound(make, n, p, [gpu] * 3, align=256).run(hp3, hg3, mode="exact")
+    assert torch.equal(hp1, hp3) and torch.equal(hg1, hg3)
+    assert not torch.equal(hg1, xg)          # the averaged gradients were written back

@@ -62,3 +62,16 @@ def test_blocked_layout_roundtrip_cpu():
     assert torch.equal(xb[1, 2, :10], x[2, 4096:4106])
     assert float(xb[2, :, 9000 - 8192:].abs().sum()) == 0.0
     assert torch.equal(memory.from_blocked(xb, 9000), x)
+
+
+def test_mixing_devices_policy(monkeypatch):
+    """One GPU per 64K parameter columns at most, NIIDMIX_DEVICES selects (no GPU needed)."""
+    import torch
+    from niidmix.slab import MIN_STRIPE_COLS, mixing_devices
+    devs = [torch.device("cuda", i) for i in range(8)]
+    assert mixing_devices(7850, devs) == devs[:1]                 # linear MNIST model
+    assert mixing_devices(62006, devs) == devs[:1]                # LeNet size
+    assert mixing_devices(1 << 20, devs) == devs                  # 1M parameters: all 8
+    assert mixing_devices(3 * MIN_STRIPE_COLS, devs) == devs[:3]
+    monkeypatch.setenv("NIIDMIX_DEVICES", "2,5")
+    assert mixing_devices(1 << 20) == [torch.device("cuda", 2), torch.device("cuda", 5)]

@@ -61,12 +61,15 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, name, p, rounds, q):
+def _worker(rank, world, port, name, p, rounds, q, topo=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import oracle
-        g = load_golden(name)
+        if topo is None:
+            g = load_golden(name)
+        else:                                   # generated topology handed over by the parent
+            g = dict(topo)
         csr = _csr(g)
 
         def compute(x2d, out2d, kernel=None, mode="exact"):
@@ -112,6 +115,37 @@ def test_gloo_sharded_rounds(world, name, oracle_mod):
     for _ in range(rounds):
         ref = oracle_mod.mix_exact_c(ref, g["row_ptr"], g["col"], g["val"])
     full = np.zeros_like(ref)
+    for rank, nodes, res in got:
+        full[nodes] = res
+    assert oracle_mod.bitwise_equal(full, ref)
+
+
+@pytest.mark.parametrize("inter", ["fully-connected", "smallworld"])
+def test_gloo_world8_dcliques10000(inter, oracle_mod):
+    """BASELINE configs[4]'s problem: 10 000 d-cliques nodes (100 cliques of 100, the reference
+    generator restated, seed 1337) over 8 node shards, halo rows exchanged over gloo (the same
+    DistTransport code the RCCL path runs), 2 rounds: bitwise the single-process oracle rounds."""
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(10000, 100, inter, 1337)
+    p, rounds, world = 12, 2, 8
+    gen = np.random.default_rng(10000)
+    x = gen.standard_normal((10000, p)).astype(np.float32)
+    topo = {"row_ptr": csr.row_ptr, "col": csr.col, "val": csr.val, "cliques": cliques, "x": x}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, None, p, rounds, q, topo))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref = x.copy()
+    for _ in range(rounds):
+        ref = oracle_mod.mix_exact_c(ref, csr.row_ptr, csr.col, csr.val)
+    full = np.full_like(ref, np.nan)
     for rank, nodes, res in got:
         full[nodes] = res
     assert oracle_mod.bitwise_equal(full, ref)

@@ -4,6 +4,7 @@ scaling, emulated one rank at a time on ONE GPU (tuning tool, not the bench): fo
 rank r's stripe of the 1000*N-node d-cliques round, timed with HIP events.
 
     python tools/stripe_probe.py [--worlds 1,2,4,8] [--steps 20] [--interclique fully-connected]
+                                 [--fixed 10000]    (strong scaling: the same N for every world)
 """
 import argparse
 import os
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--p", type=int, default=1 << 20)
     ap.add_argument("--interclique", default="fully-connected")
+    ap.add_argument("--fixed", type=int, default=0, help="fixed node count (strong scaling)")
     ap.add_argument("--variant", action="append", default=[],
                     help="name:ENV=VAL,ENV2=VAL2 (kernel-library tuning env, interleaved per rank)")
     a = ap.parse_args()
@@ -28,7 +30,8 @@ def main():
     dev = torch.device("cuda:0")
     for world in map(int, a.worlds.split(",")):
         for rank in sorted({0, world - 1}):
-            sm = StripedMixer.dcliques(1000, 100, world, rank, a.interclique, dev, a.p)
+            sm = StripedMixer.dcliques(a.fixed or 1000 * world, 100, world, rank, a.interclique,
+                                       dev, a.p)
             x = sm.empty().normal_()
             y = sm.empty()
             for rep in range(2 if a.variant else 1):
