@@ -1706,8 +1706,12 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
         !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
         (!plan->res_member && plan->n_members > 0) || !plan->csr_ptr || !plan->csr_col || !plan->csr_val)
         return set_error(NIIDMIX_EINVAL, "null pointer");
-    if (block_cols < 256 || (block_cols & (block_cols - 1)))
-        return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= 256", (long long)block_cols);
+    // the register tile's items are 256 columns wide, the big-clique kernel's 32: an item never
+    // straddles a block
+    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 256;
+    if (block_cols < min_bc || (block_cols & (block_cols - 1)))
+        return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= %lld", (long long)block_cols,
+                         (long long)min_bc);
     if (ld < block_cols) return set_error(NIIDMIX_EINVAL, "row stride < block_cols");
     if (block_stride_x < ld || block_stride_y < ld)
         return set_error(NIIDMIX_EINVAL, "block stride < row stride");

@@ -95,6 +95,22 @@ class MixCSR:
         w[self.col, dst] = self.val
         return w
 
+    def relabel(self, perm):
+        """The same operator with node i stored at slab row perm[i] (a device-resident row order,
+        e.g. clique-contiguous): row perm[i] of the result lists (perm[src], W[src, i]) in the same
+        operand order, so every output is computed exactly as before, only stored elsewhere."""
+        perm = np.asarray(perm, np.int64)
+        n = self.n
+        if self.n_in != n or sorted(perm.tolist()) != list(range(n)):
+            raise ValueError("relabel needs a permutation of the N rows (no halo rows)")
+        inv = np.empty(n, np.int64)
+        inv[perm] = np.arange(n)
+        lens = np.diff(self.row_ptr)[inv]
+        row_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        idx = np.concatenate([np.arange(self.row_ptr[i], self.row_ptr[i + 1]) for i in inv]) \
+            if n else np.zeros(0, np.int64)
+        return MixCSR(row_ptr, perm[self.col[idx]].astype(np.int32), self.val[idx].copy()).validate()
+
     def validate(self):
         n = self.n
         if self.row_ptr[0] != 0 or np.any(np.diff(self.row_ptr) < 1):
