@@ -36,6 +36,11 @@ def main():
         csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
         cliques = None
         orders = ["rank"]
+    elif a.config == "dcliques10000":
+        from niidmix.generate import dcliques_csr
+        csr, cliques = dcliques_csr(10000, 100, "fully-connected", 1337)
+        n = csr.n
+        orders = a.orders.split(",")
     else:
         g = np.load(os.path.join(REPO, "tests", "golden", "dcliques1000_fc_p64.npz"))
         csr = ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"])
