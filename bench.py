@@ -82,9 +82,10 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident round (pinned [N,P] host slab -> H2D -> mix -> "
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
-    ap.add_argument("--layout", default="blocked", choices=["blocked", "rowmajor"],
-                    help="single GPU, clique kernel: device-resident slabs column-blocked "
-                         "[P/1024, N, 1024] (default) or row-major [N, P]")
+    ap.add_argument("--layout", default="blocked", choices=["blocked", "blocked-rank", "rowmajor"],
+                    help="single GPU, clique kernel: device-resident slabs column-blocked [P/B, N, B] "
+                         "with clique-contiguous rows and B per plan (Mixer.device_layout, default), "
+                         "column-blocked [P/1024, N, 1024] in rank order, or row-major [N, P]")
     ap.add_argument("--hipmalloc-slabs", action="store_true",
                     help="single GPU: allocate the slabs with torch's default (hipMalloc) allocator "
                          "instead of the VMM-mapped slab pool")
@@ -242,9 +243,11 @@ def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
     from niidmix.generate import dcliques_csr
     csr, cliques = dcliques_csr(n, 100, interclique, 1337)
     m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
-    xa = memory.empty_blocked(n, p, dev)
+    perm, bc = m.device_layout()
+    m = m.relabeled(perm)
+    xa = memory.empty_blocked(n, p, dev, bc)
     xa.normal_(generator=torch.Generator(device=dev).manual_seed(7))
-    xb = memory.empty_blocked(n, p, dev)
+    xb = memory.empty_blocked(n, p, dev, bc)
     for _ in range(warmup):
         m.mix_blocked(xa, xb, p)
         xa, xb = xb, xa
@@ -413,13 +416,22 @@ def main():
         k0 = args.kernel
         if k0 == "auto":
             k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
-        if (args.layout == "blocked" and not args.hipmalloc_slabs and p % 4 == 0 and
-                ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 1024) or
-                 args.workload == "grad-clique")):
-            # device-resident node state in the column-blocked layout [K, N, 1024]
-            xa = memory.empty_blocked(n_local, p, dev)
+        row_order = "rank"
+        if (args.layout in ("blocked", "blocked-rank") and not args.hipmalloc_slabs and p % 4 == 0
+                and ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 1024)
+                     or args.workload == "grad-clique")):
+            # device-resident node state in the column-blocked layout [K, N, B],
+            # with the row order and block width the factored kernel streams best
+            # (Mixer.device_layout: clique-contiguous rows; B = 1024, 256 or 32 per plan)
+            bc = memory.BLOCK_COLS
+            if args.workload == "mix" and args.layout == "blocked":
+                perm, bc = mixer.device_layout()
+                if perm is not None:
+                    mixer = mixer.relabeled(perm)
+                    row_order = "clique-contiguous"
+            xa = memory.empty_blocked(n_local, p, dev, bc)
             xa.normal_(generator=gen)
-            xb = memory.empty_blocked(n_local, p, dev)
+            xb = memory.empty_blocked(n_local, p, dev, bc)
         else:
             xa = alloc()
             xa.normal_(generator=gen)
@@ -435,6 +447,7 @@ def main():
                                       mode="exact" if args.kernel.endswith("exact") else "fast")
         n_local, n_total = mixer.n_local, mixer.n_total
         cols_local, halo = mixer.p_local, 0
+        row_order = "clique-contiguous" if mixer.perm is not None else "rank"
         desc = (f"d-cliques N={n_total} ({n_total // 100} cliques x 100, {args.interclique} "
                 f"interclique, MH), P={p} split in {world} column stripes")
         parallelism = (f"{world} parameter-column stripes of all {n_total} nodes (columns "
@@ -445,6 +458,7 @@ def main():
         xa.normal_(generator=gen)
         xb = mixer.empty()
     else:
+        row_order = "shard-local (whole cliques)"
         from niidmix.shard import ShardedMixer
         p = args.p or (1 << 20)
         mixer = ShardedMixer.dcliques(n_total=n_multi, clique_size=100, world=world, rank=rank,
@@ -530,8 +544,8 @@ def main():
         region_s, launch_ms = tt.tolist()
     step_s = region_s / args.steps
     value = n_total * p * 4 / step_s / 1e9
-    slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}]"
-                   if xa.dim() == 3 and (blocked or args.shard == "stripes") else
+    slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}], "
+                   f"{row_order} rows" if xa.dim() == 3 and (blocked or args.shard == "stripes") else
                    "window-blocked [K, rows_in, w]" if xa.dim() == 3 else "row-major [N, P]")
     single = None
     if fixed and args.single_ref != "off":

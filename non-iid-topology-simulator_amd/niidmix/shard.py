@@ -377,9 +377,15 @@ class StripedMixer:
         self.mode = mode
         self.mixer = ops.Mixer(csr=csr, cliques=cliques, device=self.device)
         # column-blocked stripes whenever the factored kernels read them (register tile up to 256
-        # members, one-pass big-clique kernel up to 1024) and the plan has no cancelling terms
+        # members, one-pass big-clique kernel up to 1024) and the plan has no cancelling terms, in
+        # the device layout those kernels stream best (Mixer.device_layout: clique-contiguous rows,
+        # block width per plan): node i lives at stripe row perm[i]
         self.blocked = (mode == "fast" and self.mixer.factored_safe and
                         self.mixer.plan.max_clique <= 1024 and self.p_local % 4 == 0)
+        self.perm, self.block_cols = None, None
+        if self.blocked:
+            self.perm, self.block_cols = self.mixer.device_layout()
+            self.mixer = self.mixer.relabeled(self.perm)
 
     @classmethod
     def dcliques(cls, n_total, clique_size, world, rank, interclique, device, p, seed=1337,
@@ -391,8 +397,31 @@ class StripedMixer:
     def empty(self):
         from . import memory
         if self.blocked:
-            return memory.empty_blocked(self.n_total, self.p_local, self.device)
+            return memory.empty_blocked(self.n_total, self.p_local, self.device, self.block_cols)
         return memory.empty_slab(self.n_total, self.p_local, self.device)
+
+    def to_layout(self, x):
+        """This rank's stripe of a row-major [N, p_local] slab in rank order -> the device layout."""
+        from . import memory
+        if not self.blocked:
+            out = self.empty()
+            out.copy_(x)
+            return out
+        if self.perm is not None:
+            rows = torch.empty_like(x)
+            rows[torch.from_numpy(self.perm).to(x.device)] = x
+            x = rows
+        return memory.to_blocked(x, self.block_cols)
+
+    def from_layout(self, y):
+        """The device layout -> row-major [N, p_local] in rank order."""
+        from . import memory
+        if not self.blocked:
+            return y
+        y = memory.from_blocked(y, self.p_local)
+        if self.perm is not None:
+            y = y[torch.from_numpy(self.perm).to(y.device)]
+        return y
 
     def kernel_for(self, mode="fast", x=None):
         return "clique" if self.blocked and mode == "fast" else self.mixer.kernel_for(mode)

@@ -1,9 +1,11 @@
 """Parity of the shipped paths at the sizes they actually run (BASELINE.json configs[1..3]), through
 the same layouts and launch paths as bench.py and the drop-in:
 
-  * headline (configs[2]): the column-blocked VMM slab [1024, 1000, 1024] read directly by the clique
-    kernel, checked block by block against the oracle (no row-major round trip);
-  * fully-connected N=1000 (configs[3]): the blocked one-pass big-clique kernel at P = 2^20;
+  * headline (configs[2]): the column-blocked VMM slab [1024, 1000, 1024] (clique-contiguous rows)
+    read directly by the clique kernel, checked block by block against the oracle (no row-major
+    round trip);
+  * fully-connected N=1000 (configs[3]): the one-pass big-clique kernel on [32768, 1000, 32] at
+    P = 2^20;
   * ring N=100, P=62006 (configs[1]): the CSR kernel inside a hipGraph (bench.py's small-slab path),
     fast and exact, two ping-pong rounds per graph;
 plus the non-finite guard on the blocked and two-pass layouts, and the consensus-distance event
@@ -48,20 +50,24 @@ def _blocked_colsums(xb):
 
 
 def test_headline_blocked_vmm_slab_direct(gpu, oracle_mod):
-    """bench.py's headline round exactly as timed: VMM column-blocked slabs [1024, 1000, 1024],
-    mix_blocked (k_mix_clique<16,7,2,...>), checked on blocks 0, 511 and 1023 against the oracle
-    run on those blocks; every block's column sums are preserved (W doubly stochastic)."""
+    """bench.py's headline round exactly as timed: the device layout Mixer.device_layout picks
+    (clique-contiguous rows, VMM column-blocked slabs [1024, 1000, 1024]), mix_blocked
+    (k_mix_clique<16,7,2,...>) on the relabeled operator, checked on blocks 0, 511 and 1023 against
+    the oracle run on those blocks (relabeled CSR: the same sums, stored at permuted rows); every
+    block's column sums are preserved (W doubly stochastic)."""
     from niidmix import memory
     g, csr = _golden_csr("dcliques1000_fc_p64")
     m = _mixer(csr, g["cliques"], gpu)
-    xb = memory.empty_blocked(1000, P_FULL, gpu)
+    perm, bc = m.device_layout()
+    m = m.relabeled(perm)
+    xb = memory.empty_blocked(1000, P_FULL, gpu, bc)
     assert tuple(xb.shape) == (1024, 1000, 1024)
     xb.normal_(generator=torch.Generator(device=gpu).manual_seed(0))
-    yb = memory.empty_blocked(1000, P_FULL, gpu)
+    yb = memory.empty_blocked(1000, P_FULL, gpu, bc)
     m.mix_blocked(xb, yb, P_FULL)
     torch.cuda.synchronize()
     for k in (0, 511, 1023):
-        _check_block(oracle_mod, csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
+        _check_block(oracle_mod, m.csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
     assert torch.max(torch.abs(_blocked_colsums(xb) - _blocked_colsums(yb))).item() < 1e-3
 
 
@@ -75,12 +81,14 @@ def test_fc1000_blocked_bigclique_fullsize(gpu, oracle_mod):
     csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
     m = _mixer(csr, None, gpu)
     assert m.kernel_for("fast") == "clique" and m.plan.max_clique == 1000
-    xb = memory.empty_blocked(n, P_FULL, gpu)
+    perm, bc = m.device_layout()
+    assert perm is None and bc == 32                 # [32768, 1000, 32]: one 128 KB item per block
+    xb = memory.empty_blocked(n, P_FULL, gpu, bc)
     xb.normal_(generator=torch.Generator(device=gpu).manual_seed(1))
-    yb = memory.empty_blocked(n, P_FULL, gpu)
+    yb = memory.empty_blocked(n, P_FULL, gpu, bc)
     m.mix_blocked(xb, yb, P_FULL)
     torch.cuda.synchronize()
-    for k in (0, 600, 1023):
+    for k in (0, 1, 17000, 32767):
         _check_block(oracle_mod, csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
     assert torch.max(torch.abs(_blocked_colsums(xb) - _blocked_colsums(yb))).item() < 1e-3
 
@@ -194,3 +202,46 @@ def test_consensus_event_vs_reference_logger(name, gpu):
         np.testing.assert_allclose(got[key], want[key], rtol=1e-5, err_msg=key)
     np.testing.assert_allclose(got["std"], want["std"], rtol=1e-4)
     np.testing.assert_allclose(ev["center"]["norm"], ref["center"]["norm"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["dcliques1000_fc_p64", "nonfinite_dcliques300_fc_p64"])
+def test_device_layout_relabeled_bitwise(name, gpu):
+    """Mixer.device_layout (clique-contiguous rows, per-plan block width) + Mixer.relabeled: the
+    round on the permuted, blocked slab is bitwise the rank-order round, row for row."""
+    from niidmix import memory
+    g, csr = _golden_csr(name)
+    m = _mixer(csr, g["cliques"], gpu)
+    perm, bc = m.device_layout()
+    assert perm is not None and bc in (256, 1024)
+    mr = m.relabeled(perm)
+    p = 4096 + 256
+    x = torch.randn(m.n, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(4))
+    if "nonfinite" in name:
+        x[:, :64] = torch.from_numpy(g["x"]).to(gpu)
+    y = memory.empty_blocked(m.n, p, gpu)
+    m.mix_blocked(memory.to_blocked(x), y, p)
+    pt = torch.from_numpy(perm).to(gpu)
+    xp = torch.empty_like(x)
+    xp[pt] = x
+    yp = memory.empty_blocked(m.n, p, gpu, bc)
+    mr.mix_blocked(memory.to_blocked(xp, bc), yp, p)
+    assert torch.equal(memory.from_blocked(yp, p)[pt], memory.from_blocked(y, p))
+
+
+def test_fc_block32_layout_bitwise(gpu):
+    """Big cliques stream 32-column blocks ([P/32, N, 32]: an item is one contiguous 128 KB
+    stretch); bitwise the 1024-column layout's result, ragged last block included."""
+    from niidmix import memory
+    from niidmix.topology import mh_csr
+    n = 600
+    csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
+    m = _mixer(csr, None, gpu)
+    perm, bc = m.device_layout()
+    assert perm is None and bc == 32
+    p = 3000 + 20
+    x = torch.randn(n, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(5))
+    y1 = memory.empty_blocked(n, p, gpu, 1024)
+    m.mix_blocked(memory.to_blocked(x, 1024), y1, p)
+    y2 = memory.empty_blocked(n, p, gpu, 32)
+    m.mix_blocked(memory.to_blocked(x, 32), y2, p)
+    assert torch.equal(memory.from_blocked(y1, p), memory.from_blocked(y2, p))

@@ -124,11 +124,11 @@ def test_striped_mixer_equals_single_gpu(world, gpu, oracle_mod):
         sm = StripedMixer(csr, cliques, world, r, gpu, p)
         if sm.p_local == 0:
             continue
-        assert sm.blocked
-        xs = memory.to_blocked(x[:, sm.c0:sm.c1].contiguous())
+        assert sm.blocked and sm.perm is not None      # clique-contiguous device rows
+        xs = sm.to_layout(x[:, sm.c0:sm.c1].contiguous())
         ys = sm.empty()
         sm(xs, ys)
-        assert torch.equal(memory.from_blocked(ys, sm.p_local), y_full[:, sm.c0:sm.c1]), r
+        assert torch.equal(sm.from_layout(ys), y_full[:, sm.c0:sm.c1]), r
         covered += sm.p_local
         if r == 0:
             se = StripedMixer(csr, cliques, world, r, gpu, p, mode="exact")
