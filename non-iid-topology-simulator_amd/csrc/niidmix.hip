@@ -109,11 +109,6 @@ __device__ __forceinline__ float4 axpy4(float w, float4 xv, float4 acc) {
 // acc), y = z + acc: k_mix_csr's fast mode), which reproduces the reference's inf / NaN pattern.
 // Finite outputs are untouched; the check costs one v_cmp_class per output element.
 //   row-uniform form (one wave, V columns per lane): csr_refix;  per-lane form: csr_refix1.
-__device__ __forceinline__ bool finite4(const float *v) {
-    return __builtin_isfinite(v[0]) & __builtin_isfinite(v[1]) & __builtin_isfinite(v[2]) &
-           __builtin_isfinite(v[3]);
-}
-
 template <int V>
 __device__ __forceinline__ void csr_refix(const float *__restrict__ xc, int64_t ld_x, unsigned lo, bool act,
                                        int64_t row, const int64_t *__restrict__ rp,
@@ -344,10 +339,25 @@ template <int V> __device__ __forceinline__ void ldv_nt(const float *p, float *o
 template <> __device__ __forceinline__ void ldv_nt<4>(const float *p, float *o) {
     const float4 v = ld4_nt(p); o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
 }
+template <> __device__ __forceinline__ void ldv_nt<2>(const float *p, float *o) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p)); o[0] = v[0]; o[1] = v[1];
+}
+template <> __device__ __forceinline__ void ldv_nt<1>(const float *p, float *o) {
+    o[0] = __builtin_nontemporal_load(p);
+}
 
-// V = columns per lane per row: 4 (float4, 256-column chunks; cliques up to WAVES*RPW <= 256) or 1
-// (one float, 64-column chunks; not instantiated yet: with RPW up to 64 rows per wave the
-// compiler hoists every row address into scalar registers and spills).
+template <int V> __device__ __forceinline__ bool finite_v(const float *v) {
+    bool ok = true;
+#pragma unroll
+    for (int e = 0; e < V; ++e) ok &= __builtin_isfinite(v[e]);
+    return ok;
+}
+
+// V = columns per lane per row: 4 (float4, 256-column chunks), 2 (float2, 128) or 1 (one float, 64
+// columns).  Narrow chunks shrink a column chunk's working set (every clique's rows of that chunk)
+// so that the gateway rows one clique gathers from the others stay in the XCD's 4 MB L2: the
+// 10 000-node d-cliques round gathers ~1 gateway row per member.
 template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
@@ -361,7 +371,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     // column-blocked slabs ([K][rows][B], B = CW << cpb_shift columns, block strides bs_x / bs_y
     // floats; a row-major slab is one block: cpb_shift = 62): chunk c lives in block c >> cpb_shift
     static_assert(RPW <= 64 && RW <= 64, "one descriptor lane per register row");
-    static_assert(V == 4, "float4 per lane (V = 1 not instantiated yet)");
+    static_assert(V == 1 || V == 2 || V == 4, "1, 2 or 4 columns per lane");
+    static_assert(V == 4 || (FL & 16) == 0, "plain-store variant: float4 only");
     constexpr bool NTL = (FL & 2) != 0;       // non-temporal member-row loads (read-once stream)
     // timing-only ablations (WRONG results; instantiated only with -DNIIDMIX_ABLATIONS for
     // tools/tune_inproc.py): 4 = skip residual gathers, 8 = skip the cross-wave LDS reduction
@@ -449,6 +460,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             if (V == 4) *reinterpret_cast<float4 *>(&red[g][wave][4 * lane]) = make_float4(s[g][0], s[g][V > 1 ? 1 : 0], s[g][V > 2 ? 2 : 0], s[g][V > 3 ? 3 : 0]);
+            else if (V == 2) *reinterpret_cast<float2 *>(&red[g][wave][2 * lane]) = make_float2(s[g][0], s[g][V > 1 ? 1 : 0]);
             else red[g][wave][lane] = s[g][0];
         }
     }
@@ -546,10 +558,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 for (int e = 0; e < V; ++e) v[r][e] = __builtin_fmaf(cg, sg[g][e], v[r][e]);
             }
             const int64_t row = __builtin_amdgcn_readlane(d.row, r);
-            if (__ballot(act && !finite4(v[r]))) {
+            if (__ballot(act && !finite_v<V>(v[r]))) {
                 bad |= 1u << r;
             } else if (act) {
-                if (PLAIN_ST) *reinterpret_cast<float4 *>(yc + row * ld_y + lo) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+                if constexpr (PLAIN_ST) *reinterpret_cast<float4 *>(yc + row * ld_y + lo) = make_float4(v[r][0], v[r][V > 1 ? 1 : 0], v[r][V > 2 ? 2 : 0], v[r][V > 3 ? 3 : 0]);
                 else stv_nt<V>(yc + row * ld_y + lo, v[r]);
             }
         }
@@ -1427,8 +1439,10 @@ int64_t clique_skew() {
 }
 
 struct BlockGeom {            // column blocking of the slabs (row-major: one block)
-    int cpb_shift = 62;        // 256-column chunks per block = 1 << cpb_shift
+    int bc_shift = 70;         // block_cols = 1 << bc_shift (row-major: "infinite")
     int64_t bs_x = 0, bs_y = 0;
+    // (64*V)-column chunks per block = 1 << cpb_shift(V)
+    int cpb_shift(int v) const { return bc_shift >= 62 ? 62 : bc_shift - (v == 4 ? 8 : v == 2 ? 7 : 6); }
 };
 
 template <int WAVES, int RPW, int G, int OCC, int RW, int FL, int V>
@@ -1438,7 +1452,7 @@ void launch_clique(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t
     hipLaunchKernelGGL((k_mix_clique<WAVES, RPW, G, OCC, RW, FL, V>), dim3((unsigned)grid),
                        dim3(WAVES * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr,
                        pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col,
-                       pl->res_val, pl->res_member, n_items, clique_skew(), bg.cpb_shift, bg.bs_x,
+                       pl->res_val, pl->res_member, n_items, clique_skew(), bg.cpb_shift(V), bg.bs_x,
                        bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val);
 }
 
@@ -1459,20 +1473,23 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 }
 
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
-// targets, RW = residual entries per wave held lane-parallel (gathered in batches; more fall back
-// to a per-entry loop), FL = flags (2: non-temporal member loads), V = columns per lane (4 when the
-// slab allows float4 access and the clique fits 256 rows, else 1).
+// targets, RW = residual entries per wave held lane-parallel (gathered in batches, then further
+// chunks of 64), FL = flags (2: non-temporal member loads), V = columns per lane: 4, or the block
+// width / 64 for column blocks narrower than 256 (Mixer.device_layout picks 64-column blocks for
+// gateway-heavy plans, so that a column chunk's rows stay in L2 for the gateway gathers).
 // NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>x<v> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                         const niidmix_clique_plan *pl, bool vec4, hipStream_t s,
                         const BlockGeom &bg = BlockGeom()) {
     int waves = 0, rpw = 0, occ = 0, rw = 0, ob = 0, v = 0;
     if (const char *e = getenv("NIIDMIX_CLIQUE_TILE")) sscanf(e, "%dx%dx%dx%dx%dx%d", &waves, &rpw, &occ, &rw, &ob, &v);
-    if (v == 0) v = 4;
+    const int vmax = bg.bc_shift >= 8 ? 4 : bg.bc_shift == 7 ? 2 : 1;    // chunks never straddle blocks
+    if (v == 0) v = vmax;
+    if (v > vmax) return set_error(NIIDMIX_EINVAL, "%d columns per lane do not fit %d-column blocks", v, 1 << bg.bc_shift);
     const int mc = pl->max_clique;
     if (!vec4) return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
     if (waves * rpw < mc) {
-        rw = 64; ob = 2; v = 4;     // non-temporal member loads: 1.39 vs 1.47 ms (headline, same box)
+        rw = 64; ob = 2; v = vmax;  // non-temporal member loads: 1.39 vs 1.47 ms (headline, same box)
         if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
         else if (mc <= 32) { waves = 8; rpw = 4; occ = 8; }
         else if (mc <= 64) { waves = 16; rpw = 4; occ = 8; }
@@ -1480,10 +1497,18 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         else if (mc <= 128) { waves = 16; rpw = 8; occ = 4; }
         else if (mc <= 256) { waves = 16; rpw = 16; occ = 4; }
         else return set_error(NIIDMIX_EUNSUPPORTED, "clique of %d members > 256", mc);
+        if (v < 4) {                // narrow-chunk tiles: instantiated for the two largest shapes
+            if (mc <= 112) { waves = 16; rpw = 7; occ = 8; }
+            else if (v == 2) { waves = 16; rpw = 16; occ = 4; }
+            else return set_error(NIIDMIX_EUNSUPPORTED, "64-column blocks: cliques of <= 112 members "
+                                  "(a 16 x 16 one-float tile spills)");
+        }
     }
 #define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s, bg)
     NIIDMIX_TILE(8, 2, 8, 64, 2, 4); NIIDMIX_TILE(8, 4, 8, 64, 2, 4); NIIDMIX_TILE(16, 4, 8, 64, 2, 4);
     NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
+    NIIDMIX_TILE(16, 7, 8, 64, 2, 2); NIIDMIX_TILE(16, 16, 4, 64, 2, 2);
+    NIIDMIX_TILE(16, 7, 8, 64, 2, 1);
     // tuning alternatives (all exact-result variants; the timing-only ablations FL & 4 / FL & 8 are
     // built only with -DNIIDMIX_ABLATIONS, never into the shipped library)
     NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 7, 8, 0, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 2, 4);
@@ -1706,9 +1731,9 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
         !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
         (!plan->res_member && plan->n_members > 0) || !plan->csr_ptr || !plan->csr_col || !plan->csr_val)
         return set_error(NIIDMIX_EINVAL, "null pointer");
-    // the register tile's items are 256 columns wide, the big-clique kernel's 32: an item never
-    // straddles a block
-    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 256;
+    // the register tile's items are 64, 128 or 256 columns wide (as the block allows), the
+    // big-clique kernel's 32: an item never straddles a block
+    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 64;
     if (block_cols < min_bc || (block_cols & (block_cols - 1)))
         return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= %lld", (long long)block_cols,
                          (long long)min_bc);
@@ -1731,7 +1756,7 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
         return launch_bigclique_reg(x, ld, y, ld, p, plan, __builtin_ctzll((unsigned long long)block_cols),
                                     block_stride_x, block_stride_y, reinterpret_cast<hipStream_t>(stream));
     BlockGeom bg;
-    bg.cpb_shift = __builtin_ctzll((unsigned long long)(block_cols / 256));
+    bg.bc_shift = __builtin_ctzll((unsigned long long)block_cols);
     bg.bs_x = block_stride_x;
     bg.bs_y = block_stride_y;
     return launch_clique_tiled(x, ld, y, ld, p, plan, vec4, reinterpret_cast<hipStream_t>(stream), bg);
