@@ -60,7 +60,7 @@ def main():
             cl2 = [[int(perm[r]) for r in c] for c in cliques]
         m = ops.Mixer(csr=c2, cliques=cl2, device=dev)
         for b in map(int, a.blocks.split(",")):
-            if m.plan.max_clique <= 256 and b < 256:
+            if m.plan.max_clique <= 256 and b < 64:
                 continue
             variants.append((f"{order}/B{b}", m, b))
     res = {name: [] for name, _, _ in variants}
