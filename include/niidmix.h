@@ -153,10 +153,11 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  * (K = ceil(p / block_cols) blocks of row-major [rows, block_cols] sub-slabs with row stride `ld`
  * floats and block strides block_stride_x / block_stride_y floats), element (r, c) at
  *   base + (c / block_cols) * block_stride + r * ld + c % block_cols.
- * block_cols: a power of two >= 64 (the register tile's chunks are 64, 128 or 256 columns, as the block
- * allows), >= 32 when max_clique > 256 (the big-clique kernel's 32-column items).  This is the layout niidmix keeps device-resident node state
- * in (block_cols = 1024): a clique's member rows then sit 4 KiB apart instead of P*4 bytes, which
- * measured robust to the slab's physical placement.  Cliques of <= 256 members use
+ * block_cols: a power of two >= 256 (the register tile's 256-column chunks), >= 32 when
+ * max_clique > 256 (the big-clique kernel's 32-column items).  This is the layout niidmix keeps
+ * device-resident node state in (Mixer.device_layout: block_cols = 1024 for cliques of <= 256
+ * members, 256 when a clique has > 64 gateway terms, 32 for big cliques; clique-contiguous rows),
+ * which measured robust to the slab's physical placement.  Cliques of <= 256 members use
  * the register tile, 257..1024 members the one-pass big-clique kernel (32-column items). */
 int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t ld,
                                    int64_t block_cols, int64_t block_stride_x,

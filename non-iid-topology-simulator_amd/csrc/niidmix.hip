@@ -1474,9 +1474,10 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
 // targets, RW = residual entries per wave held lane-parallel (gathered in batches, then further
-// chunks of 64), FL = flags (2: non-temporal member loads), V = columns per lane: 4, or the block
-// width / 64 for column blocks narrower than 256 (Mixer.device_layout picks 64-column blocks for
-// gateway-heavy plans, so that a column chunk's rows stay in L2 for the gateway gathers).
+// chunks of 64), FL = flags (2: non-temporal member loads), V = columns per lane (4: 256-column
+// chunks).  Narrower chunks (V = 2 / 1, which would keep a 10 000-node chunk's rows in L2 for the
+// gateway gathers) measured far slower: too few bytes in flight per wave (10 000 nodes: 20.5 /
+// 37.9 ms vs 15.5 ms; 1000 nodes 1.57 / 2.85 vs 1.37 ms), so only V = 4 is instantiated.
 // NIIDMIX_CLIQUE_TILE=<waves>x<rpw>x<occ>x<rw>x<flags>x<v> overrides the choice (tuning only).
 int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                         const niidmix_clique_plan *pl, bool vec4, hipStream_t s,
@@ -1507,8 +1508,6 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 #define NIIDMIX_TILE(W, R, O, RWV, OB, VV) if (waves == W && rpw == R && occ == O && rw == RWV && ob == OB && v == VV) return launch_clique_g<W, R, O, RWV, OB, VV>(x, ld_x, y, ld_y, p, pl, s, bg)
     NIIDMIX_TILE(8, 2, 8, 64, 2, 4); NIIDMIX_TILE(8, 4, 8, 64, 2, 4); NIIDMIX_TILE(16, 4, 8, 64, 2, 4);
     NIIDMIX_TILE(16, 7, 8, 64, 2, 4); NIIDMIX_TILE(16, 8, 4, 64, 2, 4); NIIDMIX_TILE(16, 16, 4, 64, 2, 4);
-    NIIDMIX_TILE(16, 7, 8, 64, 2, 2); NIIDMIX_TILE(16, 16, 4, 64, 2, 2);
-    NIIDMIX_TILE(16, 7, 8, 64, 2, 1);
     // tuning alternatives (all exact-result variants; the timing-only ablations FL & 4 / FL & 8 are
     // built only with -DNIIDMIX_ABLATIONS, never into the shipped library)
     NIIDMIX_TILE(16, 7, 8, 64, 0, 4); NIIDMIX_TILE(16, 7, 8, 0, 2, 4); NIIDMIX_TILE(8, 13, 4, 64, 2, 4);
@@ -1731,9 +1730,9 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
         !plan->res_ptr || (!plan->res_col && plan->n_members > 0) || (!plan->res_val && plan->n_members > 0) ||
         (!plan->res_member && plan->n_members > 0) || !plan->csr_ptr || !plan->csr_col || !plan->csr_val)
         return set_error(NIIDMIX_EINVAL, "null pointer");
-    // the register tile's items are 64, 128 or 256 columns wide (as the block allows), the
-    // big-clique kernel's 32: an item never straddles a block
-    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 64;
+    // the register tile's items are 256 columns wide, the big-clique kernel's 32: an item never
+    // straddles a block
+    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 256;
     if (block_cols < min_bc || (block_cols & (block_cols - 1)))
         return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= %lld", (long long)block_cols,
                          (long long)min_bc);
