@@ -1,0 +1,76 @@
+#!/usr/bin/env python
+"""Exact-mode (bit-identical) round A/B on the headline topology (tuning tool, not the bench): the
+LDS-staged merged-order tile kernel at tile heights --rts, position metadata by scalar loads or
+lane-parallel v_readlane (NIIDMIX_TILE_LDS_META), interleaved in one process; results of every
+variant are checked bitwise against the first.
+
+    python tools/exact_probe.py [--rts 8,16] [--metas scalar,lanes] [--reps 2]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "non-iid-topology-simulator_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rts", default="8,16")
+    ap.add_argument("--metas", default="scalar,lanes")
+    ap.add_argument("--p", type=int, default=1 << 20)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--order", default="clique", choices=["rank", "clique"])
+    a = ap.parse_args()
+    from niidmix import memory, ops
+    dev = torch.device("cuda:0")
+    g = np.load(os.path.join(REPO, "tests", "golden", "dcliques1000_fc_p64.npz"))
+    csr = ops.csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    f, cp = g["cliques_flat"], g["cliques_ptr"]
+    cliques = [f[cp[i]:cp[i + 1]].tolist() for i in range(len(cp) - 1)]
+    base = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+    if a.order == "clique":
+        perm, _ = base.device_layout()
+        csr = csr.relabel(perm)
+        cliques = [[int(perm[r]) for r in c] for c in cliques]
+    mixers = {}
+    for rt in a.rts.split(","):
+        os.environ["NIIDMIX_TILE_LDS_RT"] = rt
+        m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+        assert m.tlds is not None, m.tlds_reason
+        mixers[int(rt)] = m
+    n = csr.n
+    x = memory.empty_slab(n, a.p, dev)
+    x.normal_(generator=torch.Generator(device=dev).manual_seed(0))
+    y = memory.empty_slab(n, a.p, dev)
+    ref = None
+    res = {}
+    for rep in range(a.reps):
+        for rt, m in mixers.items():
+            for meta in a.metas.split(","):
+                os.environ["NIIDMIX_TILE_LDS_META"] = meta
+                m(x, out=y, kernel="tile-lds-exact")
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = y[:, :65536].clone()
+                else:
+                    assert torch.equal(y[:, :65536], ref), (rt, meta)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(a.steps):
+                    m(x, out=y, kernel="tile-lds-exact")
+                e.record()
+                torch.cuda.synchronize()
+                ms = s.elapsed_time(e) / a.steps
+                res.setdefault(f"rt{rt}/{meta}", []).append(ms)
+                print(f"rep {rep} rt {rt} meta {meta}: {ms:.3f} ms", flush=True)
+    for k, v in res.items():
+        print(f"SUMMARY exact {a.order} {k}: min {min(v):.3f} ms mean {np.mean(v):.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
