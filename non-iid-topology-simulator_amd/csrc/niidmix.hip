@@ -1128,80 +1128,9 @@ __global__ __launch_bounds__(256) void k_mix_tile(
 // own order with the reference's roundings; a POS_UNIFORM position forms fl(w*x) once.
 // Work order is XCD-aware (the groups of one chunk run back to back on one XCD) so the gateway rows
 // a group stages from other cliques are that XCD's L2 hits.
-// acc[r] += tp for every tile row r except k (wave-uniform), one straight-line case per k (a
-// macro over the kernel's own acc[] so that every index is a constant: the array stays in VGPRs)
-#define NIIDMIX_ROWS_EXCEPT_8(k, acc, tp) \
-    switch (k) { \
-        case 0: acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 1: acc[0] = acc[0] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 2: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 3: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 4: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 5: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; break; \
-        case 6: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[7] = acc[7] + tp; break; \
-        case 7: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; break; \
-        default: break; \
-    }
-#define NIIDMIX_ROWS_EXCEPT_16(k, acc, tp) \
-    switch (k) { \
-        case 0: acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 1: acc[0] = acc[0] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 2: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 3: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 4: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 5: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 6: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 7: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 8: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 9: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 10: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 11: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 12: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 13: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; break; \
-        case 14: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[15] = acc[15] + tp; break; \
-        case 15: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; break; \
-        default: break; \
-    }
-#define NIIDMIX_ROWS_EXCEPT_32(k, acc, tp) \
-    switch (k) { \
-        case 0: acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 1: acc[0] = acc[0] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 2: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 3: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 4: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 5: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 6: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 7: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 8: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 9: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 10: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 11: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 12: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 13: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 14: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 15: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 16: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 17: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 18: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 19: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 20: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 21: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 22: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 23: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 24: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 25: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 26: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 27: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 28: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 29: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[30] = acc[30] + tp; acc[31] = acc[31] + tp; break; \
-        case 30: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[31] = acc[31] + tp; break; \
-        case 31: acc[0] = acc[0] + tp; acc[1] = acc[1] + tp; acc[2] = acc[2] + tp; acc[3] = acc[3] + tp; acc[4] = acc[4] + tp; acc[5] = acc[5] + tp; acc[6] = acc[6] + tp; acc[7] = acc[7] + tp; acc[8] = acc[8] + tp; acc[9] = acc[9] + tp; acc[10] = acc[10] + tp; acc[11] = acc[11] + tp; acc[12] = acc[12] + tp; acc[13] = acc[13] + tp; acc[14] = acc[14] + tp; acc[15] = acc[15] + tp; acc[16] = acc[16] + tp; acc[17] = acc[17] + tp; acc[18] = acc[18] + tp; acc[19] = acc[19] + tp; acc[20] = acc[20] + tp; acc[21] = acc[21] + tp; acc[22] = acc[22] + tp; acc[23] = acc[23] + tp; acc[24] = acc[24] + tp; acc[25] = acc[25] + tp; acc[26] = acc[26] + tp; acc[27] = acc[27] + tp; acc[28] = acc[28] + tp; acc[29] = acc[29] + tp; acc[30] = acc[30] + tp; break; \
-        default: break; \
-    }
-
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
-template <bool EXACT, int RT, int SV, bool SMETA>
+template <bool EXACT, int RT, int SV>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
@@ -1269,64 +1198,6 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             acc[r] = axpy2<EXACT>(ws, xs, xs * 0.f);
         }
         const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
-        if constexpr (SMETA) {
-            // position metadata by SCALAR loads (wave-uniform addresses: no v_readlane), D positions
-            // per batch; a FULL mask is RT packed adds, an all-rows-but-one mask (a tile row's own
-            // member position) RT-1 adds through for_rows_except, other masks per-row selects
-            for (int64_t k = beg; k < end; k += D) {
-                int sw[D];
-                uint32_t mk[D];
-                float wu[D];
-#pragma unroll
-                for (int u = 0; u < D; ++u) {
-                    const int64_t kk = k + u < end ? k + u : end - 1;
-                    sw[u] = pos_slot[kk];
-                    mk[u] = pos_mask[kk];
-                    wu[u] = pos_w[kk * RT];
-                }
-                f2 xv[D];
-#pragma unroll
-                for (int u = 0; u < D; ++u) xv[u] = stage[(sw[u] & kPosRowMask) * 64 + lane];
-#pragma unroll
-                for (int u = 0; u < D; ++u) {
-                    if (k + u >= end) break;                                // wave-uniform
-                    const uint32_t m = mk[u];
-                    if ((sw[u] & kPosUniform) != 0) {
-                        const float w = wu[u];
-                        const f2 x2 = xv[u];
-                        const f2 tp = x2 * w;                 // exact: one product for the tile
-                        if (m == FULL) {
-#pragma unroll
-                            for (int r = 0; r < RT; ++r) {
-                                if constexpr (EXACT) acc[r] = acc[r] + tp;
-                                else acc[r] = axpy2<false>(w, x2, acc[r]);
-                            }
-                        } else if (EXACT && __builtin_popcount(m) == RT - 1) {
-                            // all rows but one (a tile row's own member position: a node is not in
-                            // its own edge list): RT-1 adds in the straight-line case of the skipped
-                            // row, no per-row selects
-                            const int ks = __builtin_ctz(~m);
-                            if constexpr (RT == 8) { NIIDMIX_ROWS_EXCEPT_8(ks, acc, tp) }
-                            else if constexpr (RT == 16) { NIIDMIX_ROWS_EXCEPT_16(ks, acc, tp) }
-                            else { NIIDMIX_ROWS_EXCEPT_32(ks, acc, tp) }
-                        } else if constexpr (EXACT) {
-#pragma unroll
-                            for (int r = 0; r < RT; ++r)
-                                if ((m >> r) & 1u) acc[r] = acc[r] + tp;            // wave-uniform
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < RT; ++r)
-                                if ((m >> r) & 1u) acc[r] = axpy2<false>(w, x2, acc[r]);
-                        }
-                    } else {
-                        const float *wp = pos_w + (k + u) * RT;
-#pragma unroll
-                        for (int r = 0; r < RT; ++r)
-                            if ((m >> r) & 1u) acc[r] = axpy2<EXACT>(wp[r], xv[u], acc[r]);
-                    }
-                }
-            }
-        } else
         for (int64_t kb = beg; kb < end; kb += 64) {
             // 64 positions' (slot, mask, uniform weight) fetched lane-parallel and handed out by
             // v_readlane: the position loop issues no scalar or global loads (only per-row weights
@@ -2021,12 +1892,8 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
     const size_t lds = (size_t)plan->max_src * 128 * sizeof(float);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
-    // position metadata by scalar loads + all-but-one masks without selects (default) or the
-    // lane-parallel v_readlane form (NIIDMIX_TILE_LDS_META=lanes, A/B)
-    const char *meta_env = getenv("NIIDMIX_TILE_LDS_META");
-    const bool smeta = !(meta_env && !strcmp(meta_env, "lanes"));
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = smeta ? k_mix_tile_lds<E, R, V, true> : k_mix_tile_lds<E, R, V, false>; \
+        auto kfn = k_mix_tile_lds<E, R, V>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
         hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rts", default="8,16")
-    ap.add_argument("--metas", default="scalar,lanes")
+    ap.add_argument("--metas", default="lanes")
     ap.add_argument("--p", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=2)
