@@ -15,7 +15,8 @@ roofline: the dominant kernel's algorithmic bytes per launch (read Θ once + wri
 around every launch in the timed region), against the 8.0 TB/s HBM3E peak (MI355X_MICROARCH.md).
 Dense W (fully-connected) is priced in FLOPs (2*N^2*P) against the 157.3 TF fp32 MFMA peak.
 traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x2 on gfx950 + WRITE_SIZE)
-read from --traffic-json (produced by tools in profiles/), else null.
+read from --traffic-json (tools/pmc_traffic.py, keyed by config.traffic_key), reported only when the
+entry was measured with the library this run loaded (config.lib_sha16), else null.
 
 cpu_baseline (rank 0, N=1): the reference loop restated faithfully in torch CPU
 (oracle.reference_loop_average: per-node deepcopy / mul_(0) / add_(w*p), then update_models) timed
@@ -236,6 +237,10 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
     return res
 
 
+def traffic_key(args, kernel, p, slab_layout):
+    return f"{args.config}/{args.workload}/{kernel}/p{p}/{slab_layout}"
+
+
 def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
     """One GPU, the whole d-cliques problem of n nodes: the headline kernel on column-blocked VMM
     slabs (2 x n*p*4 bytes), mean of `steps` rounds after `warmup`."""
@@ -265,12 +270,20 @@ def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
     return ms
 
 
-def load_traffic(path, key):
+def load_traffic(path, key, lib_sha):
+    """PMC bytes per launch for `key` from profiles/traffic.json (tools/pmc_traffic.py), only if the
+    entry was measured with THIS library (lib_sha16 stamp); else (None, why)."""
     try:
         with open(path) as f:
-            return json.load(f).get(key)
+            e = json.load(f).get("entries", {}).get(key)
     except (OSError, ValueError):
-        return None
+        return None, "no traffic file"
+    if e is None:
+        return None, f"no PMC entry for {key}"
+    if e.get("lib_sha16") != lib_sha:
+        return None, f"PMC entry stale (measured with library {e.get('lib_sha16')}, loaded {lib_sha})"
+    return float(e["bytes"]), "PMC (FETCH_SIZE x2 + WRITE_SIZE) of this library, profiles/traffic.json"
+
 
 
 def cpu_baseline(csr, p, sample_nodes):
@@ -559,8 +572,12 @@ def main():
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
     if rank == 0:
-        # PMC traffic is profiled per single-GPU config (profiles/traffic.json)
-        traffic = load_traffic(args.traffic_json, f"{args.config}/{kernel}/p{p}") if world == 1 else None
+        # PMC traffic is profiled per single-GPU config and library build (profiles/traffic.json)
+        from niidmix import _lib
+        lib_sha = _lib.lib_sha16()
+        traffic, traffic_src = (load_traffic(args.traffic_json, traffic_key(args, kernel, p,
+                                                                            slab_layout), lib_sha)
+                                if world == 1 else (None, "multi-GPU: not profiled"))
         if kernel == "dense":
             flops = 2.0 * n_local * n_local * cols_local
             achieved = flops / (launch_ms / 1e3) / 1e12
@@ -600,6 +617,8 @@ def main():
                                        (world > 1 and args.shard == "nodes")
                                        else "VMM 2 MiB chunks (niidmix_hbm_alloc)"),
                        "slab_layout": slab_layout,
+                       "lib_sha16": lib_sha, "traffic_source": traffic_src,
+                       "traffic_key": traffic_key(args, kernel, p, slab_layout),
                        "stream_copy_GBs": round(copy_gbs, 1),
                        "frac_of_stream_copy": (round(roof["achieved"] / copy_gbs, 4)
                                                if roof["unit"] == "GB/s" else None)},

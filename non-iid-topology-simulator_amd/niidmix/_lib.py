@@ -74,6 +74,14 @@ SIGNATURES = {
 }
 
 
+def lib_sha16(path=None):
+    """First 16 hex digits of the SHA-256 of the loaded library: identifies the kernels a
+    measurement (e.g. a PMC traffic entry in profiles/traffic.json) was taken with."""
+    import hashlib
+    with open(path or LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 class NiidmixError(RuntimeError):
     pass
 

@@ -2,6 +2,9 @@
 """Per-launch HBM traffic of a kernel from rocprofv3 PMC passes (measurement tool).
 
     python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR [--key K --out profiles/traffic.json]
+                                [--alg-bytes B]
+Entries are stamped with the SHA-256 (16 hex digits) of the library the run loaded; bench.py only
+reports an entry whose stamp matches the library it loads (a kernel change makes it stale).
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (summed over the TCC instances).  On gfx950
 FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read
@@ -39,7 +42,14 @@ def main():
     ap.add_argument("--key")
     ap.add_argument("--out")
     ap.add_argument("--alg-bytes", type=float, default=None)
+    ap.add_argument("--lib", default=None, help="library the profiled run loaded (default: in-tree)")
+    ap.add_argument("--key-from", default=None,
+                    help="take --key from config.traffic_key of this bench.py JSON output")
     a = ap.parse_args()
+    if a.key_from:
+        with open(a.key_from) as fh:
+            line = [ln for ln in fh if ln.startswith("{")][-1]
+        a.key = json.loads(line)["config"]["traffic_key"]
     f = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     w = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
     if not f or not w:
@@ -53,12 +63,19 @@ def main():
         res["ratio_to_algorithmic"] = tot / a.alg_bytes
     print(json.dumps(res))
     if a.out and a.key:
-        data = {}
+        # entries are keyed by config/kernel/p/layout and stamped with the library they were
+        # measured with: bench.py reports an entry only while the loaded library has that hash
+        import hashlib
+        lib = a.lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "non-iid-topology-simulator_amd", "niidmix", "libniidmix.so")
+        with open(lib, "rb") as fh:
+            res["lib_sha16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
+        data = {"entries": {}}
         if os.path.exists(a.out):
             with open(a.out) as fh:
                 data = json.load(fh)
-        data[a.key] = tot
-        data.setdefault("_details", {})[a.key] = res
+            data.setdefault("entries", {})
+        data["entries"][a.key] = res
         with open(a.out, "w") as fh:
             json.dump(data, fh, indent=1, sort_keys=True)
 
