@@ -215,6 +215,7 @@ class _Engine:
         csr = to_csr(topology)
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        self.devices = devices
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
         self.runner = MultiDeviceRound(
             lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
@@ -225,9 +226,28 @@ class _Engine:
         self.runner.run(self.slab.host, mode=mode, timing=timing)
         return self.runner.last_timing
 
+    def owns(self, nodes):
+        return self.slab.owns([n["model"] for n in nodes])
+
     def valid_for(self, nodes, topology):
         return (topology is self.topology and id(topology.get("weights")) == self.weights_id
-                and self.slab.owns([n["model"] for n in nodes]))
+                and self.owns(nodes))
+
+    def set_topology(self, topology):
+        """A new topology for the same nodes (random-graph --randomize, d_sgd.py:223-234): only the
+        mixing operator is rebuilt; the pinned slab (the models' parameters) and the device window
+        buffers are kept."""
+        from .ops import Mixer
+        csr = to_csr(topology)
+        if csr.n != self.slab.n:
+            raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=self.devices[0])
+        for runner in self.runner.runners:
+            if runner is not None:
+                runner.mixer = self.mixer if runner.device == self.devices[0] else \
+                    self.mixer.to(runner.device)
+        self.topology = topology
+        self.weights_id = id(topology.get("weights"))
 
 
 
@@ -248,6 +268,8 @@ def average(nodes, topology, params):
     logging.info("  computing averages of models (GPU, %s)", _mode(params))
     key = id(nodes)
     eng = _engines.get(key)
+    if eng is not None and not eng.valid_for(nodes, topology) and eng.owns(nodes):
+        eng.set_topology(topology)                   # same nodes, new graph: keep the slab
     if eng is None or not eng.valid_for(nodes, topology):
         eng = _Engine(nodes, topology, _devices(nodes))
         _engines.clear()
@@ -326,6 +348,36 @@ def get_sample(state, params, step):
         return active
 
 
+DENSE_JSON_MAX = int(os.environ.get("NIIDMIX_DENSE_JSON_MAX", 1024))
+
+
+def randomized_topology(nodes, params, rundir):
+    """The next round's random graph (d_sgd.py:223-234: random_graph.generate_topology with the
+    incremented topology-seed), built SPARSE: the edge lists by the restated generator
+    (niidmix.generate.random_graph, same RNG order, hence the same graph) and the MH weights as a
+    CSR (topology.mh_csr, bit-identical to compute_weights) -- O(N k) weights instead of the dense
+    N x N matrix.  The rundir gets topology.csr.npz every round, and the reference's dense
+    topology.json as well up to NIIDMIX_DENSE_JSON_MAX nodes (default 1024; niidmix.topology.load
+    reads whichever is newer)."""
+    from .generate import random_graph_csr
+    from .topology import save_csr
+    t = params["topology"]
+    weights = t.get("weights", "metropolis-hasting")
+    if weights != "metropolis-hasting":
+        raise ValueError(f"--weights {weights}: only metropolis-hasting is supported (the "
+                         "reference's equal-clique-probability indexes sets, weights.py:5-14)")
+    n = len(nodes)
+    assert [nd["rank"] for nd in nodes] == list(range(n)), "nodes must be listed in rank order"
+    csr, edges = random_graph_csr(n, t["nb-neighbours"], t["topology-seed"])
+    if rundir is not None:
+        save_csr(os.path.join(rundir, "topology.csr.npz"), csr)
+        if n <= DENSE_JSON_MAX:
+            with open(os.path.join(rundir, "topology.json"), "w+") as f:
+                json.dump({"edges": {r: edges[r] for r in edges},
+                           "weights": csr.dense().tolist()}, f)
+    return {"edges": edges, "csr": csr, "weights": None}
+
+
 def next_step(state, params, rundir):
     sample = params["topology"]["name"] == "sample"
     active = get_sample(state, params, state["step"]) if sample else state["nodes"]
@@ -355,13 +407,7 @@ def next_step(state, params, rundir):
             average(active, topology, params)             # ★ GPU
         if params["topology"]["name"] == "random-graph" and params["topology"]["randomize"]:
             params["topology"]["topology-seed"] += 1
-            from setup.topology.random_graph import generate_topology   # reference generator
-            fresh = generate_topology(state["nodes"], params)
-            with open(os.path.join(rundir, "topology.json"), "w+") as f:
-                json.dump(fresh, f)
-            fresh["edges"] = {int(r): fresh["edges"][r] for r in fresh["edges"]}
-            fresh["weights"] = torch.tensor(fresh["weights"])
-            state["topology"] = fresh
+            state["topology"] = randomized_topology(state["nodes"], params, rundir)
     else:
         for n in active:
             n["optimizer"].step()

@@ -39,15 +39,17 @@ def load_file(path):
 
 def load(rundir):
     """Drop-in for setup.topology.load(rundir).  If the rundir holds a sparse companion
-    (topology.csr.npz, written by save_csr) and no dense topology.json, the sparse form is returned
-    under topology['csr'] with 'edges' rebuilt from it."""
+    (topology.csr.npz, written by save_csr / niidmix.sparse_topology) that is newer than
+    topology.json (or there is no topology.json), the sparse form is returned under
+    topology['csr'] (weights None) with 'edges' rebuilt from it."""
     path = os.path.join(rundir, "topology.json")
-    if os.path.exists(path):
-        return load_file(path)
     sparse = os.path.join(rundir, "topology.csr.npz")
+    if os.path.exists(path) and not (os.path.exists(sparse) and
+                                     os.path.getmtime(sparse) > os.path.getmtime(path)):
+        return load_file(path)
     if os.path.exists(sparse):
         csr, cliques = load_csr(sparse)
-        topo = {"edges": csr.edges(), "csr": csr}
+        topo = {"edges": csr.edges(), "csr": csr, "weights": None}
         if cliques is not None:
             topo["cliques"] = cliques
         return topo

@@ -13,11 +13,24 @@ from niidmix import generate
     ("dcliques1000_smallworld_p16", 1000, 100, "smallworld"),
     ("dcliques1000_ring_p16", 1000, 100, "ring"),
     ("dcliques300_fc_p37", 300, 30, "fully-connected"),
+    ("dcliques200_fractal_rm5_p40", 200, 20, "fractal"),
 ])
 def test_matches_reference_generator(name, n, size, inter):
     g = load_golden(name)
-    csr, cliques = generate.dcliques_csr(n, size, inter, seed=1337)
+    csr, cliques = generate.dcliques_csr(n, size, inter, seed=1337,
+                                         remove=5 if "_rm5" in name else 0)
     assert cliques == g["cliques"]
+    np.testing.assert_array_equal(csr.row_ptr, g["row_ptr"])
+    np.testing.assert_array_equal(csr.col, g["col"])
+    assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))
+
+
+def test_random_graph_matches_reference():
+    """random_graph.create + compute_weights (random_graph.py:10-51), restated sparse: the same edge
+    lists and MH weights, bit for bit, as the reference-run fixture (topology-seed 1, 5
+    neighbours)."""
+    g = load_golden("randomgraph50_p24")
+    csr, edges = generate.random_graph_csr(50, 5, 1)
     np.testing.assert_array_equal(csr.row_ptr, g["row_ptr"])
     np.testing.assert_array_equal(csr.col, g["col"])
     assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))

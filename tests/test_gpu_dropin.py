@@ -330,3 +330,33 @@ def test_multi_device_fused_round_bitwise(gpu):
     MultiDeviceRound(make, n, p, [gpu] * 3, align=256).run(hp3, hg3, mode="exact")
     assert torch.equal(hp1, hp3) and torch.equal(hg1, hg3)
     assert not torch.equal(hg1, xg)          # the averaged gradients were written back
+
+
+def test_randomize_keeps_slab(gpu, oracle_mod):
+    """--randomize: a new graph every round (d_sgd.py:223-234).  The drop-in rebuilds only the
+    mixing operator for the same nodes (the pinned slab and the device window buffers stay), and
+    each round is bit-identical to the reference loop on that round's graph."""
+    from niidmix import d_sgd, generate
+    n, p = 40, 300
+    torch.manual_seed(2)
+    nodes = [{"rank": r, "model": torch.nn.Linear(p - 1, 1)} for r in range(n)]
+    params = {"algorithm": {"mixing-mode": "exact"},
+              "topology": {"name": "random-graph", "nb-neighbours": 4, "topology-seed": 3,
+                           "weights": "metropolis-hasting", "randomize": True}}
+    topo = d_sgd.randomized_topology(nodes, params, None)
+    slab = None
+    for _ in range(3):
+        before = np.stack([torch.cat([q.detach().reshape(-1) for q in nd["model"].parameters()]).numpy()
+                           for nd in nodes])
+        d_sgd.average(nodes, topo, params)
+        eng = next(iter(d_sgd._engines.values()))
+        if slab is None:
+            slab = eng.slab
+        assert eng.slab is slab                       # same pinned slab every round
+        csr = topo["csr"]
+        after = np.stack([torch.cat([q.detach().reshape(-1) for q in nd["model"].parameters()]).numpy()
+                          for nd in nodes])
+        ref = oracle_mod.mix_exact_c(before, csr.row_ptr, csr.col, csr.val)
+        assert oracle_mod.bitwise_equal(after, ref)
+        params["topology"]["topology-seed"] += 1
+        topo = d_sgd.randomized_topology(nodes, params, None)

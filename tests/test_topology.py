@@ -70,3 +70,67 @@ def test_validation_errors():
 def test_load_missing(tmp_path):
     with pytest.raises(FileNotFoundError):
         T.load(str(tmp_path))
+
+
+def _rundir(tmp_path, n, seed, classes=10):
+    import json
+    (tmp_path / "nodes.json").write_text(json.dumps([{"rank": r} for r in range(n)]))
+    (tmp_path / "params.json").write_text(json.dumps({"meta": {"seed": seed, "log": "WARNING"},
+                                                      "dataset": {"nb-classes": classes}}))
+    return str(tmp_path)
+
+
+def test_sparse_topology_cli_dcliques(tmp_path):
+    """python -m niidmix.sparse_topology d-cliques writes topology.csr.npz holding exactly the
+    reference generator's topology (cliques, edge order, MH weights bit for bit) and the same
+    params.json 'topology' section as random_cliques.py; niidmix.topology.load reads it back."""
+    import json
+    from niidmix import sparse_topology, topology
+    rd = _rundir(tmp_path, 300, 1337)
+    sparse_topology.main(["d-cliques", "--rundir", rd, "--max-clique-size", "30"])
+    t = topology.load(rd)
+    g = load_golden("dcliques300_fc_p37")
+    csr = topology.to_csr(t)
+    np.testing.assert_array_equal(csr.row_ptr, g["row_ptr"])
+    np.testing.assert_array_equal(csr.col, g["col"])
+    assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))
+    assert t["cliques"] == g["cliques"]
+    sec = json.loads((tmp_path / "params.json").read_text())["topology"]
+    assert sec == {"name": "d-cliques/random-cliques", "weights": "metropolis-hasting",
+                   "interclique-topology": "fully-connected", "max-clique-size": 30,
+                   "remove-clique-edges": 0}
+
+
+def test_sparse_topology_cli_random_graph(tmp_path):
+    from niidmix import sparse_topology, topology
+    rd = _rundir(tmp_path, 50, 1)
+    sparse_topology.main(["random-graph", "--rundir", rd, "--nb-neighbours", "5"])
+    csr = topology.to_csr(topology.load(rd))
+    g = load_golden("randomgraph50_p24")
+    np.testing.assert_array_equal(csr.col, g["col"])
+    assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))
+
+
+def test_randomized_topology_sparse_and_dense_files(tmp_path, monkeypatch):
+    """--randomize's per-round graph (d_sgd.py:223-234) built sparse: topology.csr.npz every round,
+    the reference's dense topology.json too below NIIDMIX_DENSE_JSON_MAX nodes; both load to the
+    same CSR, and the loader takes the newer file."""
+    import os
+    import time
+    from niidmix import d_sgd, generate, topology
+    rd = str(tmp_path)
+    nodes = [{"rank": r} for r in range(60)]
+    params = {"topology": {"name": "random-graph", "nb-neighbours": 6, "topology-seed": 8,
+                           "weights": "metropolis-hasting", "randomize": True}}
+    t = d_sgd.randomized_topology(nodes, params, rd)
+    ref, _ = generate.random_graph_csr(60, 6, 8)
+    assert np.array_equal(topology.to_csr(t).val, ref.val) and t["weights"] is None
+    dense = topology.to_csr(topology.load_file(os.path.join(rd, "topology.json")))
+    np.testing.assert_array_equal(dense.col, ref.col)
+    assert np.array_equal(dense.val.view(np.uint32), ref.val.view(np.uint32))
+    monkeypatch.setattr(d_sgd, "DENSE_JSON_MAX", 10)
+    time.sleep(0.01)
+    params["topology"]["topology-seed"] = 9
+    d_sgd.randomized_topology(nodes, params, rd)            # sparse file only: newer than the JSON
+    got = topology.to_csr(topology.load(rd))
+    np.testing.assert_array_equal(got.col, generate.random_graph_csr(60, 6, 9)[0].col)
