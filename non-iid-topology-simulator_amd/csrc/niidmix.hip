@@ -1137,7 +1137,8 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int32_t *__restrict__ grp_src_rows, const int64_t *__restrict__ sub_ptr,
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
-    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
+    float neg_zero) {
     constexpr int64_t CW = 128;                  // columns per item: 64 lanes x 2
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                         // positions read together
@@ -1207,6 +1208,9 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             const int d_src = pos_slot[kb + lj];
             const int d_mask = (int)pos_mask[kb + lj];
             const int d_wu = __float_as_int(pos_w[(kb + lj) * RT]);
+            // per-chunk bit sets (one ballot each) instead of per-position v_readlane tests
+            const uint64_t full_bits = __ballot(lane < cnt && (uint32_t)d_mask == FULL);
+            const uint64_t uni_bits = __ballot(lane < cnt && (d_src & kPosUniform) != 0);
             // LDS reads double-buffered: batch j+D is read while batch j is applied
             f2 xa[D], xb[D];
 #pragma unroll
@@ -1221,29 +1225,38 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     if (j + u >= cnt) break;
-                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
-                    const bool uni = (__builtin_amdgcn_readlane(d_src, j + u) & kPosUniform) != 0;
+                    const bool uni = ((uni_bits >> (j + u)) & 1ull) != 0;
+                    const bool full = ((full_bits >> (j + u)) & 1ull) != 0;
                     if (uni) {
                         const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, j + u));
                         if (EXACT) {
                             const f2 tp = xa[u] * w;              // one product for the tile
-                            if (m == FULL) {
+                            if (full) {
 #pragma unroll
                                 for (int r = 0; r < RT; ++r) acc[r] = acc[r] + tp;
                             } else {
+                                // partial mask: every row adds tp or -0.0 (x + (-0.0) == x for
+                                // every x, so skipped rows keep their bits).  neg_zero comes from
+                                // the host so the compiler cannot fold the add into a select, which
+                                // would give every path new registers and a copy per row at the
+                                // merge: here every row is updated in place on both paths.
+                                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                                const f2 nz = {neg_zero, neg_zero};
 #pragma unroll
                                 for (int r = 0; r < RT; ++r)
-                                    if ((m >> r) & 1u) acc[r] = acc[r] + tp;      // wave-uniform
+                                    acc[r] = acc[r] + (((m >> r) & 1u) ? tp : nz);
                             }
-                        } else if (m == FULL) {
+                        } else if (full) {
 #pragma unroll
                             for (int r = 0; r < RT; ++r) acc[r] = axpy2<false>(w, xa[u], acc[r]);
                         } else {
+                            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
 #pragma unroll
                             for (int r = 0; r < RT; ++r)
                                 if ((m >> r) & 1u) acc[r] = axpy2<false>(w, xa[u], acc[r]);
                         }
                     } else {
+                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
                         const float *wp = pos_w + (kb + j + u) * RT;
 #pragma unroll
                         for (int r = 0; r < RT; ++r)
@@ -1896,7 +1909,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         auto kfn = k_mix_tile_lds<E, R, V>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, -0.0f); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)
