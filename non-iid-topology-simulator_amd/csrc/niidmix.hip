@@ -1141,6 +1141,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     float neg_zero) {
     constexpr int64_t CW = 128;                  // columns per item: 64 lanes x 2
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
+    constexpr int D = 4;                         // positions read together
     extern __shared__ float lds_tile[];          // [n_src][64] column pairs
     f2 *stage = reinterpret_cast<f2 *>(lds_tile);
     const int lane = threadIdx.x & (kWave - 1);
@@ -1210,50 +1211,60 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             // per-chunk bit sets (one ballot each) instead of per-position v_readlane tests
             const uint64_t full_bits = __ballot(lane < cnt && (uint32_t)d_mask == FULL);
             const uint64_t uni_bits = __ballot(lane < cnt && (d_src & kPosUniform) != 0);
-            // one position per iteration; the next position's LDS read is issued before this one
-            // is applied (a rotating register pair once the loop is unrolled by 2: no copies)
-            f2 xn = stage[(__builtin_amdgcn_readlane(d_src, 0) & kPosRowMask) * 64 + lane];
-#pragma unroll 2
-            for (int jj = 0; jj < cnt; ++jj) {
-                const f2 xc = xn;
-                const int jn = jj + 1 < cnt ? jj + 1 : jj;
-                xn = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * 64 + lane];
-                const bool uni = ((uni_bits >> jj) & 1ull) != 0;
-                const bool full = ((full_bits >> jj) & 1ull) != 0;
-                if (uni) {
-                    const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, jj));
-                    if (EXACT) {
-                        const f2 tp = xc * w;                 // one product for the tile
-                        if (full) {
+            // LDS reads double-buffered: batch j+D is read while batch j is applied
+            f2 xa[D], xb[D];
 #pragma unroll
-                            for (int r = 0; r < RT; ++r) acc[r] = acc[r] + tp;
+            for (int u = 0; u < D; ++u)
+                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * 64 + lane];
+            for (int j = 0; j < cnt; j += D) {
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    const int jn = j + D + u < cnt ? j + D + u : cnt - 1;
+                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * 64 + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    if (j + u >= cnt) break;
+                    const bool uni = ((uni_bits >> (j + u)) & 1ull) != 0;
+                    const bool full = ((full_bits >> (j + u)) & 1ull) != 0;
+                    if (uni) {
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, j + u));
+                        if (EXACT) {
+                            const f2 tp = xa[u] * w;              // one product for the tile
+                            if (full) {
+#pragma unroll
+                                for (int r = 0; r < RT; ++r) acc[r] = acc[r] + tp;
+                            } else {
+                                // partial mask: every row adds tp or -0.0 (x + (-0.0) == x for
+                                // every x, so skipped rows keep their bits).  neg_zero comes from
+                                // the host so the compiler cannot fold the add into a select, which
+                                // would give every path new registers and a copy per row at the
+                                // merge: here every row is updated in place on both paths.
+                                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                                const f2 nz = {neg_zero, neg_zero};
+#pragma unroll
+                                for (int r = 0; r < RT; ++r)
+                                    acc[r] = acc[r] + (((m >> r) & 1u) ? tp : nz);
+                            }
+                        } else if (full) {
+#pragma unroll
+                            for (int r = 0; r < RT; ++r) acc[r] = axpy2<false>(w, xa[u], acc[r]);
                         } else {
-                            // partial mask: every row adds tp or -0.0 (x + (-0.0) == x for every
-                            // x, so skipped rows keep their bits).  neg_zero comes from the host so
-                            // the compiler cannot fold the add into a select (which would give the
-                            // paths different registers and a copy per row at the merge)
-                            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, jj);
-                            const f2 nz = {neg_zero, neg_zero};
+                            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
 #pragma unroll
                             for (int r = 0; r < RT; ++r)
-                                acc[r] = acc[r] + (((m >> r) & 1u) ? tp : nz);
+                                if ((m >> r) & 1u) acc[r] = axpy2<false>(w, xa[u], acc[r]);
                         }
-                    } else if (full) {
-#pragma unroll
-                        for (int r = 0; r < RT; ++r) acc[r] = axpy2<false>(w, xc, acc[r]);
                     } else {
-                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, jj);
+                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                        const float *wp = pos_w + (kb + j + u) * RT;
 #pragma unroll
                         for (int r = 0; r < RT; ++r)
-                            if ((m >> r) & 1u) acc[r] = axpy2<false>(w, xc, acc[r]);
+                            if ((m >> r) & 1u) acc[r] = axpy2<EXACT>(wp[r], xa[u], acc[r]);
                     }
-                } else {
-                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, jj);
-                    const float *wp = pos_w + (kb + jj) * RT;
-#pragma unroll
-                    for (int r = 0; r < RT; ++r)
-                        if ((m >> r) & 1u) acc[r] = axpy2<EXACT>(wp[r], xc, acc[r]);
                 }
+#pragma unroll
+                for (int u = 0; u < D; ++u) xa[u] = xb[u];
             }
         }
         // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc)
