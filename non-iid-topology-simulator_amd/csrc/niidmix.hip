@@ -1128,6 +1128,92 @@ __global__ __launch_bounds__(256) void k_mix_tile(
 // own order with the reference's roundings; a POS_UNIFORM position forms fl(w*x) once.
 // Work order is XCD-aware (the groups of one chunk run back to back on one XCD) so the gateway rows
 // a group stages from other cliques are that XCD's L2 hits.
+// A tile's RT accumulator pairs as register vectors of at most 16 pairs, so a row picked by a
+// wave-uniform (SGPR) index is addressed through the GPR-index moves (s_set_gpr_idx_on + v_mov)
+// instead of a select over every row (a 64-float vector would be indexed through scratch: RT 32
+// keeps two halves and picks one by a uniform branch).
+template <int RT>
+struct TileAcc {
+    static constexpr int H = RT < 16 ? RT : 16;
+    typedef float V __attribute__((ext_vector_type(2 * H)));
+    V v[RT / H];
+    __device__ __forceinline__ f2 get(int r) const {
+        if constexpr (RT <= 16) {
+            return (f2){v[0][2 * r], v[0][2 * r + 1]};
+        } else {
+            if (r < H) return (f2){v[0][2 * r], v[0][2 * r + 1]};
+            return (f2){v[1][2 * (r - H)], v[1][2 * (r - H) + 1]};
+        }
+    }
+    // every row += t (one v_pk_add_f32 per row, in place)
+    __device__ __forceinline__ void add_all(f2 t) {
+        V tv;
+#pragma unroll
+        for (int i = 0; i < H; ++i) { tv[2 * i] = t.x; tv[2 * i + 1] = t.y; }
+#pragma unroll
+        for (int h = 0; h < RT / H; ++h) v[h] = v[h] + tv;
+    }
+    // every row = fma(w, x, row)
+    __device__ __forceinline__ void fma_all(float w, f2 x) {
+        V wv, xv;
+#pragma unroll
+        for (int i = 0; i < H; ++i) { wv[2 * i] = w; wv[2 * i + 1] = w; xv[2 * i] = x.x; xv[2 * i + 1] = x.y; }
+#pragma unroll
+        for (int h = 0; h < RT / H; ++h) v[h] = __builtin_elementwise_fma(wv, xv, v[h]);
+    }
+    __device__ __forceinline__ void set(int r, f2 a) {
+        if constexpr (RT <= 16) {
+            v[0][2 * r] = a.x;
+            v[0][2 * r + 1] = a.y;
+        } else if (r < H) {
+            v[0][2 * r] = a.x;
+            v[0][2 * r + 1] = a.y;
+        } else {
+            v[1][2 * (r - H)] = a.x;
+            v[1][2 * (r - H) + 1] = a.y;
+        }
+    }
+};
+static_assert(sizeof(TileAcc<32>) == 64 * sizeof(float), "two halves of 16 pairs");
+
+// Apply op(acc_row, r) to the rows of the wave-uniform mask m.  No per-row select: on gfx950 a lane
+// mask or SGPR operand that a SALU op just wrote stalls the VALU ~30-40 cycles per row
+// (tools/valu_probe.hip: the select form of a partial position cost ~10x a full one).  Instead,
+// when one or two rows skip the position (a tile row is never its own source, so most partial
+// masks miss exactly one row) those rows are saved, every row is updated and the saved registers
+// are written back — bit-exact, the skipped rows keep their bits; sparser masks visit only their
+// rows by dynamic register index.
+template <int RT, class Op>
+__device__ __forceinline__ void apply_mask(TileAcc<RT> &acc, uint32_t m, Op op) {
+    constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
+    if (m == FULL) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc.set(r, op(acc.get(r), r));
+        return;
+    }
+    const uint32_t miss = ~m & FULL;                // != 0: the mask is not full
+    const uint32_t rest = miss & (miss - 1u);
+    if ((rest & (rest - 1u)) == 0u) {
+        const int r0 = __builtin_ctz(miss), r1 = rest ? __builtin_ctz(rest) : r0;
+        const f2 s0 = acc.get(r0), s1 = acc.get(r1);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc.set(r, op(acc.get(r), r));
+        acc.set(r1, s1);
+        acc.set(r0, s0);
+    } else {
+        for (uint32_t b = m & FULL; b; b &= b - 1u) {
+            const int r = __builtin_ctz(b);
+            acc.set(r, op(acc.get(r), r));
+        }
+    }
+}
+
+// Time-split switch for tuning builds only (tools/tlds_split.sh builds variant libraries): 1 skips
+// the position loop, 2 skips the staging; 3-5 strip the position loop down (3: every position full
+// and uniform, 4: no product either, 5: no adds).  Product builds leave it 0.
+#ifndef NIIDMIX_TLDS_SPLIT
+#define NIIDMIX_TLDS_SPLIT 0
+#endif
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
 template <bool EXACT, int RT, int SV>
@@ -1137,8 +1223,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int32_t *__restrict__ grp_src_rows, const int64_t *__restrict__ sub_ptr,
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
-    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
-    float neg_zero) {
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
     constexpr int64_t CW = 128;                  // columns per item: 64 lanes x 2
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                         // positions read together
@@ -1154,7 +1239,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int64_t c0 = chunk * CW;
     if (c0 >= p) return;                         // block-uniform; no barrier reached yet
     // 1. stage the group's source rows: SV floats per piece, pieces of one row are contiguous
-    {
+    if (NIIDMIX_TLDS_SPLIT != 2) {
         constexpr int PPR = (int)(CW / SV);      // pieces per row
         const int s0 = grp_src_ptr[grp], ns = grp_src_ptr[grp + 1] - s0;
         const int total = ns * PPR;
@@ -1191,15 +1276,16 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const int d_row = sub_rows[sub * RT + li];
         const int d_slot = sub_slot[sub * RT + li];
         const float d_ws = sub_wself[sub * RT + li];
-        f2 acc[RT];
+        TileAcc<RT> acc;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
             const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
-            acc[r] = axpy2<EXACT>(ws, xs, xs * 0.f);
+            acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
         }
+        const bool pad_slot = __builtin_amdgcn_readlane(d_row, RT - 1) < 0;   // slot RT-1 unused
         const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
-        for (int64_t kb = beg; kb < end; kb += 64) {
+        for (int64_t kb = beg; NIIDMIX_TLDS_SPLIT != 1 && kb < end; kb += 64) {
             // 64 positions' (slot, mask, uniform weight) fetched lane-parallel and handed out by
             // v_readlane: the position loop issues no scalar or global loads (only per-row weights
             // of a non-uniform position are read from pos_w)
@@ -1209,7 +1295,58 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             const int d_mask = (int)pos_mask[kb + lj];
             const int d_wu = __float_as_int(pos_w[(kb + lj) * RT]);
             // per-chunk bit sets (one ballot each) instead of per-position v_readlane tests
-            const uint64_t full_bits = __ballot(lane < cnt && (uint32_t)d_mask == FULL);
+            // A chunk whose positions are all SIMPLE — uniform weight, taken by every tile row but
+            // at most one (d_skip; the pad slot RT-1 when every row takes it) — runs a loop with no
+            // per-position test: save the skipped row, update every row, restore it (bit-exact).
+            // A tile row is never its own source, so a clique tile's partial positions are exactly
+            // its rows' own positions: with a pad slot (tiles of <= RT-1 rows, niidmix.tile) most
+            // chunks are simple.  Other chunks (and 32-row tiles, whose two register halves make
+            // the dynamic row index a branch) test each position (apply_mask).
+            const uint32_t miss = ~(uint32_t)d_mask & FULL;
+            const bool simple = (d_src & kPosUniform) != 0 && (miss & (miss - 1u)) == 0u && (miss != 0u || pad_slot);
+            if (RT <= 16 && __ballot(lane < cnt && !simple) == 0) {
+                // one position: save the skipped row, update all rows in place, restore it.  Every
+                // per-position value comes by v_readlane from the chunk's lanes (lanes >= cnt hold
+                // copies of the last position, and v_readlane wraps its lane index at 64, so the
+                // prefetch reads past the end need no clamping: fewer SALU ops per position).
+                const int d_skip = miss ? __builtin_ctz(miss) : RT - 1;
+                auto step = [&](int jj, f2 xu) {
+                    const int r0 = __builtin_amdgcn_readlane(d_skip, jj);
+                    const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, jj));
+                    const f2 keep = acc.get(r0);
+                    if (EXACT) {
+                        f2 tp = xu * w;                           // one product for the tile
+                        asm("" : "+v"(tp));                       // kept as one pair, not re-formed per row
+                        acc.add_all(tp);
+                    } else {
+                        acc.fma_all(w, xu);
+                    }
+                    acc.set(r0, keep);
+                };
+                const int d_addr = (d_src & kPosRowMask) * 64 + lane;   // LDS f2 index per position
+                // groups of D positions with the LDS reads of the next group in flight; no exit
+                // inside a group (an early exit would give every exit its own register copy)
+                const int nd = cnt & ~(D - 1);
+                f2 xa[D], xb[D];
+#pragma unroll
+                for (int u = 0; u < D; ++u)
+                    xa[u] = stage[__builtin_amdgcn_readlane(d_addr - lane, u) + lane];
+                for (int j = 0; j < nd; j += D) {
+#pragma unroll
+                    for (int u = 0; u < D; ++u)
+                        xb[u] = stage[__builtin_amdgcn_readlane(d_addr - lane, j + D + u) + lane];
+#pragma unroll
+                    for (int u = 0; u < D; ++u) step(j + u, xa[u]);
+#pragma unroll
+                    for (int u = 0; u < D; ++u) xa[u] = xb[u];
+                }
+                for (int j = nd; j < cnt; ++j)                    // the chunk's last cnt % D
+                    step(j, stage[__builtin_amdgcn_readlane(d_addr - lane, j) + lane]);
+                continue;
+            }
+            // the uniform flag as one ballot per chunk; the mask comes by v_readlane and is tested
+            // by SALU compares only (a bool kept as a lane mask would cost a SALU->VALU mask
+            // round trip per position)
             const uint64_t uni_bits = __ballot(lane < cnt && (d_src & kPosUniform) != 0);
             // LDS reads double-buffered: batch j+D is read while batch j is applied
             f2 xa[D], xb[D];
@@ -1225,42 +1362,30 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     if (j + u >= cnt) break;
-                    const bool uni = ((uni_bits >> (j + u)) & 1ull) != 0;
-                    const bool full = ((full_bits >> (j + u)) & 1ull) != 0;
-                    if (uni) {
+                    const f2 xu = xa[u];
+                    if constexpr (NIIDMIX_TLDS_SPLIT >= 3) {   // tuning builds: loop-cost decomposition
+                        f2 tp = xu;
+                        if (NIIDMIX_TLDS_SPLIT == 3) tp = xu * __int_as_float(__builtin_amdgcn_readlane(d_wu, j + u));
+                        asm("" : "+v"(tp));
+                        if (NIIDMIX_TLDS_SPLIT == 5) acc.set(0, acc.get(0) + tp);
+                        else
+#pragma unroll
+                            for (int r = 0; r < RT; ++r) acc.set(r, acc.get(r) + tp);
+                        continue;
+                    }
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
+                    if ((uni_bits >> (j + u)) & 1ull) {
                         const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, j + u));
                         if (EXACT) {
-                            const f2 tp = xa[u] * w;              // one product for the tile
-                            if (full) {
-#pragma unroll
-                                for (int r = 0; r < RT; ++r) acc[r] = acc[r] + tp;
-                            } else {
-                                // partial mask: every row adds tp or -0.0 (x + (-0.0) == x for
-                                // every x, so skipped rows keep their bits).  neg_zero comes from
-                                // the host so the compiler cannot fold the add into a select, which
-                                // would give every path new registers and a copy per row at the
-                                // merge: here every row is updated in place on both paths.
-                                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
-                                const f2 nz = {neg_zero, neg_zero};
-#pragma unroll
-                                for (int r = 0; r < RT; ++r)
-                                    acc[r] = acc[r] + (((m >> r) & 1u) ? tp : nz);
-                            }
-                        } else if (full) {
-#pragma unroll
-                            for (int r = 0; r < RT; ++r) acc[r] = axpy2<false>(w, xa[u], acc[r]);
+                            f2 tp = xu * w;                       // one product for the tile
+                            asm("" : "+v"(tp));                   // kept as one pair, not re-formed per row
+                            apply_mask<RT>(acc, m, [&](f2 a, int) { return a + tp; });
                         } else {
-                            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
-#pragma unroll
-                            for (int r = 0; r < RT; ++r)
-                                if ((m >> r) & 1u) acc[r] = axpy2<false>(w, xa[u], acc[r]);
+                            apply_mask<RT>(acc, m, [&](f2 a, int) { return axpy2<false>(w, xu, a); });
                         }
                     } else {
-                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j + u);
                         const float *wp = pos_w + (kb + j + u) * RT;
-#pragma unroll
-                        for (int r = 0; r < RT; ++r)
-                            if ((m >> r) & 1u) acc[r] = axpy2<EXACT>(wp[r], xa[u], acc[r]);
+                        apply_mask<RT>(acc, m, [&](f2 a, int r) { return axpy2<EXACT>(wp[r], xu, a); });
                     }
                 }
 #pragma unroll
@@ -1272,10 +1397,10 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         for (int r = 0; r < RT; ++r) {
             const int row = __builtin_amdgcn_readlane(d_row, r);
             if (row < 0) continue;                                  // wave-uniform
-            f2 o = acc[r];
+            f2 o = acc.get(r);
             if (!avg_only) {
                 const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
-                o = xs * 0.f + acc[r];
+                o = xs * 0.f + o;
             }
             if (ok) {
                 float *dst = y + (int64_t)row * ld_y + col;
@@ -1909,7 +2034,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         auto kfn = k_mix_tile_lds<E, R, V>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, -0.0f); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)

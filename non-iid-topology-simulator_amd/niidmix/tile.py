@@ -12,6 +12,7 @@ Density = entries / (rt * positions) is the fraction of useful (row, position) w
 picks the tile kernel when it is high (cliques: ~0.8-0.9; a ring: ~0.1 -> CSR gather instead).
 """
 import bisect
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -137,7 +138,7 @@ def _split(rows, rt):
     return parts
 
 
-def _class_tiles(group, rp, val, rt):
+def _class_tiles(group, rp, val, rt, max_rows=None):
     """Tiles of a row group: rows ordered by degree — under Metropolis-Hastings the weight
     W[j, i] = 1/(max(d_i, d_j) + 1) a source j carries into row i depends on i only through d_i —
     and each degree class cut on its own, so a source's weight is the same across a tile's rows
@@ -161,10 +162,10 @@ def _class_tiles(group, rp, val, rt):
             merged.append(list(run))
     if len(merged) > 1 and len(merged[-1]) < small:
         merged[-2].extend(merged.pop())
-    return [part for run in merged for part in _split(run, rt)]
+    return [part for run in merged for part in _split(run, max_rows or rt)]
 
 
-def build_tile_plan(csr, groups=None, rt=16):
+def build_tile_plan(csr, groups=None, rt=16, max_rows=None):
     """(plan, None) or (None, reason).  groups: row lists (e.g. the cliques) cut into tiles of <= rt
     rows; None -> consecutive rows.  Every CSR row must belong to exactly one group.
 
@@ -172,7 +173,7 @@ def build_tile_plan(csr, groups=None, rt=16):
     tile holds rows of one Metropolis-Hastings degree class (D-Cliques: the gateway rows together):
     the weights a source carries into a tile's rows are then equal, the position is flagged
     POS_UNIFORM and the exact kernel forms each product once for the whole tile (its weight is
-    replicated into every slot of pos_w)."""
+    replicated into every slot of pos_w).  max_rows (<= rt) caps the rows a tile holds."""
     if rt not in TILE_ROWS:
         return None, f"rt={rt} not in {TILE_ROWS}"
     n = csr.n
@@ -187,7 +188,7 @@ def build_tile_plan(csr, groups=None, rt=16):
     pos_src, pos_mask, pos_w = [], [], []
     grp_tile_ptr = [0]
     for g in groups:
-        for part in _class_tiles(g, rp, val, rt):
+        for part in _class_tiles(g, rp, val, rt, max_rows):
             lists = [(col[rp[r] + 1:rp[r + 1]], val[rp[r] + 1:rp[r + 1]]) for r in part]
             pad = full & ~((1 << len(part)) - 1)
             for c, mask, ws in _merge(lists):
@@ -255,7 +256,14 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
             n_src = len(np.unique(np.concatenate([col[idx], g])))
             if n_src > LDS_MAX_SRC:
                 return None, f"group {gi} reads {n_src} distinct rows (> {LDS_MAX_SRC})"
-    tp, why = build_tile_plan(csr, groups, rt)
+    # tiles of at most rt-1 rows leave slot rt-1 unused: the kernel's branch-free loop skips that
+    # pad slot at positions every row takes (k_mix_tile_lds, "simple" chunks); when that costs more
+    # tiles than a group may have, full-height tiles (correct, slower)
+    max_rows = rt - 1 if os.environ.get("NIIDMIX_TILE_LDS_PAD", "1") == "1" else rt
+    if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.val, rt, max_rows)) > LDS_MAX_WAVES[rt]
+                      for g in groups):
+        max_rows = rt
+    tp, why = build_tile_plan(csr, groups, rt, max_rows)
     if tp is None:
         return None, why
     row_mask = POS_UNIFORM - 1

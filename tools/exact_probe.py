@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--order", default="clique", choices=["rank", "clique"])
+    ap.add_argument("--no-check", action="store_true", help="phase-split builds: results are not the mix")
     a = ap.parse_args()
     from niidmix import memory, ops
     dev = torch.device("cuda:0")
@@ -57,7 +58,7 @@ def main():
                 torch.cuda.synchronize()
                 if ref is None:
                     ref = y[:, :65536].clone()
-                else:
+                elif not a.no_check:
                     assert torch.equal(y[:, :65536], ref), (rt, meta)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()

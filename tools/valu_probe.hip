@@ -1,0 +1,143 @@
+// VALU issue-cost probe (tuning tool): cycles per wave-instruction per SIMD for the instruction
+// shapes the exact tile kernel's position loop is made of — v_pk_add_f32, v_add_f32, v_cndmask_b32,
+// v_mov_b32 and the s_set_gpr_idx save/restore of one accumulator pair — at several waves/SIMD.
+//   hipcc --offload-arch=gfx950 -O3 -o valu_probe tools/valu_probe.hip && ./valu_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f32v __attribute__((ext_vector_type(32)));
+constexpr int ITERS = 4096;
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k(float *out, float w, int sel) {
+    f32v acc;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc[i] = (float)(threadIdx.x + i);
+    f2 tp = {w, w * 2.f};
+    float nz = -0.0f * w;
+    const int idxv = (int)(threadIdx.x * 7 + sel) & 1023;
+    for (int it = 0; it < ITERS; ++it) {
+        asm volatile("" : "+v"(tp));
+        if (KIND == 0) {            // 16 v_pk_add_f32
+            f32v T = __builtin_shufflevector(tp, tp, 0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1);
+            acc = acc + T;
+        } else if (KIND == 1) {     // 32 v_add_f32
+#pragma unroll
+            for (int i = 0; i < 32; ++i) { float t = tp.x; asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[i]) : "v"(t)); }
+        } else if (KIND == 2) {     // 16 v_pk_add_f32 via asm
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { f2 a = {acc[2*i], acc[2*i+1]}; asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a) : "v"(tp)); acc[2*i] = a.x; acc[2*i+1] = a.y; }
+        } else if (KIND == 3) {     // 32 v_cndmask + 16 pk_add (select path)
+            const int m = __builtin_amdgcn_readfirstlane(sel + it);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                f2 t = ((m >> i) & 1) ? tp : (f2){nz, nz};
+                f2 a = {acc[2*i], acc[2*i+1]}; a = a + t; acc[2*i] = a.x; acc[2*i+1] = a.y;
+            }
+        } else if (KIND == 4) {     // 16 pk_add + gpr-idx save/restore of one pair
+            const int r0 = __builtin_amdgcn_readfirstlane((sel + it) & 15);
+            float s0 = acc[2 * r0], s1 = acc[2 * r0 + 1];
+            f32v T = __builtin_shufflevector(tp, tp, 0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1);
+            acc = acc + T;
+            acc[2 * r0] = s0; acc[2 * r0 + 1] = s1;
+        } else if (KIND == 5) {     // 32 v_mov
+#pragma unroll
+            for (int i = 0; i < 32; ++i) { float t = tp.x; asm volatile("v_mov_b32 %0, %1" : "=v"(acc[i]) : "v"(t)); }
+        } else if (KIND == 6) {     // 16 v_pk_mul_f32 via asm
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { f2 a = {acc[2*i], acc[2*i+1]}; asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a) : "v"(tp)); acc[2*i] = a.x; acc[2*i+1] = a.y; }
+        } else if (KIND == 7) {     // 16 v_pk_fma_f32 via asm
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { f2 a = {acc[2*i], acc[2*i+1]}; asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(a) : "v"(tp)); acc[2*i] = a.x; acc[2*i+1] = a.y; }
+        } else if (KIND == 10) {    // as 4, the index from a v_readlane (VALU -> SALU dependency)
+            const int r0 = __builtin_amdgcn_readlane(idxv, it & 63) & 15;
+            float s0 = acc[2 * r0], s1 = acc[2 * r0 + 1];
+            f32v T = __builtin_shufflevector(tp, tp, 0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1);
+            acc = acc + T;
+            acc[2 * r0] = s0; acc[2 * r0 + 1] = s1;
+        } else if (KIND == 11) {    // 16 pk_add + a v_readlane feeding a SALU compare + branch
+            const int m = __builtin_amdgcn_readlane(idxv, it & 63);
+            f32v T = __builtin_shufflevector(tp, tp, 0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1);
+            if (m == 12345) acc[0] += 1.f;
+            acc = acc + T;
+        } else if (KIND == 12 || KIND == 13) {   // 16 pk_add, and a uniform SGPR-bit branch around a 2-move save/restore
+            const uint64_t bits = KIND == 12 ? 0x8040201008040201ull : 0ull;
+            f32v T = __builtin_shufflevector(tp, tp, 0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1,0,1);
+            const uint64_t bb = (uint64_t)__builtin_amdgcn_readfirstlane(sel) | bits;
+            if ((bb >> (it & 63)) & 1ull) {
+                const int r0 = (it * 5) & 15;
+                float s0 = acc[2 * r0], s1 = acc[2 * r0 + 1];
+                acc = acc + T;
+                acc[2 * r0] = s0; acc[2 * r0 + 1] = s1;
+            } else {
+                acc = acc + T;
+            }
+        } else if (KIND == 8) {     // select by bit-field insert, SALU row mask: 16 s_bfe + 32 v_bfi + 16 pk_add
+            const int m = __builtin_amdgcn_readfirstlane(sel + it);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                int mr;
+                asm volatile("s_bfe_i32 %0, %1, %2" : "=s"(mr) : "s"(m), "i"((1 << 16) | i));
+                f2 t;
+                asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(t.x) : "s"(mr), "v"(tp.x), "v"(nz));
+                asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(t.y) : "s"(mr), "v"(tp.y), "v"(nz));
+                f2 a = {acc[2*i], acc[2*i+1]}; a = a + t; acc[2*i] = a.x; acc[2*i+1] = a.y;
+            }
+        } else if (KIND == 9) {     // same, row mask by VALU: 16 v_bfe + 32 v_bfi + 16 pk_add
+            const int m = __builtin_amdgcn_readfirstlane(sel + it);
+            int vm = m;
+            asm volatile("" : "+v"(vm));
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                int mr;
+                asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(mr) : "v"(vm), "i"(i));
+                f2 t;
+                asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(t.x) : "v"(mr), "v"(tp.x), "v"(nz));
+                asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(t.y) : "v"(mr), "v"(tp.y), "v"(nz));
+                f2 a = {acc[2*i], acc[2*i+1]}; a = a + t; acc[2*i] = a.x; acc[2*i+1] = a.y;
+            }
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += acc[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+static const char *names[] = {"16 pk_add (compiler)", "32 v_add_f32", "16 pk_add (asm)", "select path: 32 cndmask + 16 pk_add",
+                              "16 pk_add + gpr_idx save/restore", "32 v_mov", "16 pk_mul (asm)", "16 pk_fma (asm)",
+                              "bfi select, SALU mask: 32 v_bfi + 16 pk_add", "bfi select, VALU mask: 16 v_bfe + 32 v_bfi + 16 pk_add",
+                              "16 pk_add + gpr_idx, index by v_readlane", "16 pk_add + v_readlane->s_cmp->branch",
+                              "16 pk_add, SGPR-bit branch, 1/8 save/restore", "16 pk_add, SGPR-bit branch never taken"};
+static const int instrs[] = {16, 32, 16, 48, 16, 32, 16, 16, 48, 64, 16, 16, 16, 16};
+
+template <int KIND>
+void run(float *out, int blocks_per_cu) {
+    int cus = 256;
+    int blocks = cus * blocks_per_cu;                 // 4 waves per block -> blocks_per_cu waves/SIMD
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a);
+    hipEventRecord(a);
+    for (int r = 0; r < 5; ++r) k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    ms /= 5;
+    // wave-instructions per SIMD = waves/SIMD * ITERS * instrs
+    double per_simd = (double)blocks_per_cu * ITERS * instrs[KIND];
+    double cyc = ms * 1e-3 * 2.4e9;
+    printf("%-40s waves/SIMD %2d: %.3f ms, %.2f cyc/instr @2.4GHz (%.1f cyc per loop iteration per wave)\n",
+           names[KIND], blocks_per_cu, ms, cyc / per_simd, cyc / (blocks_per_cu * (double)ITERS));
+}
+
+int main() {
+    float *out;
+    hipMalloc(&out, 256 * 16 * 256 * sizeof(float));
+    for (int occ : {2, 4, 8}) {
+        run<0>(out, occ); run<4>(out, occ); run<12>(out, occ); run<13>(out, occ);
+    }
+    hipFree(out);
+    return 0;
+}
