@@ -1295,25 +1295,18 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             const int d_mask = (int)pos_mask[kb + lj];
             const int d_wu = __float_as_int(pos_w[(kb + lj) * RT]);
             // per-chunk bit sets (one ballot each) instead of per-position v_readlane tests
-            // A chunk whose positions are all SIMPLE — uniform weight, taken by every tile row but
-            // at most one (d_skip; the pad slot RT-1 when every row takes it) — runs a loop with no
-            // per-position test: save the skipped row, update every row, restore it (bit-exact).
-            // A tile row is never its own source, so a clique tile's partial positions are exactly
-            // its rows' own positions: with a pad slot (tiles of <= RT-1 rows, niidmix.tile) most
-            // chunks are simple.  Other chunks (and 32-row tiles, whose two register halves make
-            // the dynamic row index a branch) test each position (apply_mask).
+            // A SIMPLE position — uniform weight, taken by every tile row but at most one (d_skip;
+            // the pad slot RT-1 when every row takes it) — needs no per-position test: save the
+            // skipped row, update every row, restore it (bit-exact).  A tile row is never its own
+            // source, so a clique tile's partial positions are mostly its rows' own positions: with
+            // a pad slot (tiles of <= RT-1 rows, niidmix.tile) most positions are simple.  32-row
+            // tiles (two register halves make the dynamic row index a branch) test each position.
             const uint32_t miss = ~(uint32_t)d_mask & FULL;
             const bool simple = (d_src & kPosUniform) != 0 && (miss & (miss - 1u)) == 0u && (miss != 0u || pad_slot);
-            if (RT <= 16 && __ballot(lane < cnt && !simple) == 0) {
-                // one position: save the skipped row, update all rows in place, restore it.  Every
-                // per-position value comes by v_readlane from the chunk's lanes (lanes >= cnt hold
-                // copies of the last position, and v_readlane wraps its lane index at 64, so the
-                // prefetch reads past the end need no clamping: fewer SALU ops per position).
+            if (RT <= 16 && NIIDMIX_TLDS_SPLIT == 0) {
                 const int d_skip = miss ? __builtin_ctz(miss) : RT - 1;
-                auto step = [&](int jj, f2 xu) {
-                    const int r0 = __builtin_amdgcn_readlane(d_skip, jj);
-                    const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, jj));
-                    const f2 keep = acc.get(r0);
+                // SIMPLE position: save the skipped row, update all rows in place, restore it
+                auto update = [&](float w, f2 xu) {
                     if (EXACT) {
                         f2 tp = xu * w;                           // one product for the tile
                         asm("" : "+v"(tp));                       // kept as one pair, not re-formed per row
@@ -1321,27 +1314,68 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     } else {
                         acc.fma_all(w, xu);
                     }
+                };
+                auto step = [&](int jj, f2 xu) {
+                    const int r0 = __builtin_amdgcn_readlane(d_skip, jj);
+                    const float w = __int_as_float(__builtin_amdgcn_readlane(d_wu, jj));
+                    const f2 keep = acc.get(r0);
+                    update(w, xu);
                     acc.set(r0, keep);
                 };
-                const int d_addr = (d_src & kPosRowMask) * 64 + lane;   // LDS f2 index per position
+                // every row takes it: no save/restore
+                auto step_full = [&](int jj, f2 xu) {
+                    update(__int_as_float(__builtin_amdgcn_readlane(d_wu, jj)), xu);
+                };
+                // any other position (a row taking it alone, a source two rows order differently,
+                // a per-row weight; rare): visit only the mask's rows, by dynamic register index
+                const uint64_t uni_bits = __ballot(lane < cnt && (d_src & kPosUniform) != 0);
+                auto general = [&](int jj, f2 xu) {
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, jj) & FULL;
+                    const bool uni = ((uni_bits >> jj) & 1ull) != 0;
+                    const float wu = __int_as_float(__builtin_amdgcn_readlane(d_wu, jj));
+                    const float *wp = pos_w + (kb + jj) * RT;
+                    for (uint32_t b = m; b; b &= b - 1u) {
+                        const int r = __builtin_ctz(b);
+                        acc.set(r, axpy2<EXACT>(uni ? wu : wp[r], xu, acc.get(r)));
+                    }
+                };
                 // groups of D positions with the LDS reads of the next group in flight; no exit
-                // inside a group (an early exit would give every exit its own register copy)
+                // inside a group (an early exit would give every exit its own register copy); SGPR
+                // bit tests per group pick the form: all D full (no save/restore), all D simple
+                const uint64_t slow_bits = __ballot(lane < cnt && !simple);
+                const uint64_t part_bits = slow_bits | __ballot(lane < cnt && miss != 0u);
+                const int d_addr = (d_src & kPosRowMask) * 64;   // LDS f2 index of each position
                 const int nd = cnt & ~(D - 1);
                 f2 xa[D], xb[D];
 #pragma unroll
                 for (int u = 0; u < D; ++u)
-                    xa[u] = stage[__builtin_amdgcn_readlane(d_addr - lane, u) + lane];
+                    xa[u] = stage[__builtin_amdgcn_readlane(d_addr, u) + lane];
                 for (int j = 0; j < nd; j += D) {
 #pragma unroll
                     for (int u = 0; u < D; ++u)
-                        xb[u] = stage[__builtin_amdgcn_readlane(d_addr - lane, j + D + u) + lane];
+                        xb[u] = stage[__builtin_amdgcn_readlane(d_addr, j + D + u) + lane];
+                    constexpr uint64_t GM = (1ull << D) - 1ull;
+                    if (((part_bits >> j) & GM) == 0ull) {        // all D taken by every row
 #pragma unroll
-                    for (int u = 0; u < D; ++u) step(j + u, xa[u]);
+                        for (int u = 0; u < D; ++u) step_full(j + u, xa[u]);
+                    } else if (((slow_bits >> j) & GM) == 0ull) {
+#pragma unroll
+                        for (int u = 0; u < D; ++u) step(j + u, xa[u]);   // full ones skip the pad
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < D; ++u) {
+                            if ((slow_bits >> (j + u)) & 1ull) general(j + u, xa[u]);
+                            else step(j + u, xa[u]);
+                        }
+                    }
 #pragma unroll
                     for (int u = 0; u < D; ++u) xa[u] = xb[u];
                 }
-                for (int j = nd; j < cnt; ++j)                    // the chunk's last cnt % D
-                    step(j, stage[__builtin_amdgcn_readlane(d_addr - lane, j) + lane]);
+                for (int j = nd; j < cnt; ++j) {                  // the chunk's last cnt % D
+                    const f2 xu = stage[__builtin_amdgcn_readlane(d_addr, j) + lane];
+                    if ((slow_bits >> j) & 1ull) general(j, xu);
+                    else step(j, xu);
+                }
                 continue;
             }
             // the uniform flag as one ballot per chunk; the mask comes by v_readlane and is tested
