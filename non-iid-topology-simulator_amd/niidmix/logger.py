@@ -10,7 +10,6 @@ The uniform average is bit-identical to setup.model.average(models) (exact kerne
 accumulated in fp64 (the reference accumulates fp32 per tensor), so they agree to ~1e-6 relative.
 """
 import json
-import math
 import statistics
 import time
 
@@ -46,17 +45,3 @@ def install(logger_class):
     logger_class.log_consensus_distance = log_consensus_distance
     return logger_class
 
-
-def reference_statistics(models):
-    """CPU restatement of the reference's arithmetic (for tests): fp32 center, per-tensor fp32
-    squared sums, sqrt of their sum."""
-    import torch
-    with torch.no_grad():
-        flat = [torch.cat([q.detach().reshape(-1) for q in m.parameters()]) for m in models]
-        k = len(flat)
-        w = float(1. / k)
-        center = flat[0] * 0
-        for f in flat:
-            center = center + w * f
-        d = [math.sqrt(float(torch.sum((center - f) ** 2))) for f in flat]
-        return d, math.sqrt(float(torch.sum(center ** 2)))

@@ -252,13 +252,27 @@ def test_sgd_step_rows_matches_torch_cpu_sgd(gpu):
     assert torch.equal(pd.cpu(), ref)
 
 
+def _cpu_consensus_statistics(models):
+    """CPU restatement of the reference's arithmetic (logger.py:257-284): fp32 center, per-tensor
+    fp32 squared sums, sqrt of their sum."""
+    import math
+    with torch.no_grad():
+        flat = [torch.cat([q.detach().reshape(-1) for q in m.parameters()]) for m in models]
+        w = float(1. / len(flat))
+        center = flat[0] * 0
+        for f in flat:
+            center = center + w * f
+        d = [math.sqrt(float(torch.sum((center - f) ** 2))) for f in flat]
+        return d, math.sqrt(float(torch.sum(center ** 2)))
+
+
 def test_consensus_distance_event(gpu, tmp_path):
     """The GPU consensus-distance event has the reference's schema and statistics."""
     from niidmix import logger as nl
     torch.manual_seed(3)
     nodes = [{"rank": i, "model": torch.nn.Linear(50, 7)} for i in range(12)]
     ev = nl.consensus_distance_event({"nodes": nodes, "step": 4})
-    d, norm = nl.reference_statistics([n["model"] for n in nodes])
+    d, norm = _cpu_consensus_statistics([n["model"] for n in nodes])
     import statistics
     g = ev["distance_to_center"]["global"]
     np.testing.assert_allclose(g["avg"], statistics.mean(d), rtol=1e-5)
