@@ -141,3 +141,34 @@ def test_striped_mixer_equals_single_gpu(world, gpu, oracle_mod):
                                          csr.val)
             assert oracle_mod.bitwise_equal(ye.cpu().numpy(), ref)
     assert covered == p
+
+
+def test_striped_mixer_bigclique_blocked(gpu):
+    """Fully-connected topology (one clique of 600 > 256 members: the one-pass big-clique kernel on
+    32-column blocks): every rank's blocked column stripe is bitwise the single-GPU blocked round's
+    columns (stripes use the blocked layout up to the 1024-member limit)."""
+    from niidmix import memory
+    from niidmix.ops import Mixer
+    from niidmix.shard import StripedMixer
+    from niidmix.topology import mh_csr
+    n, world, p = 600, 4, 4 * 2048 + 96
+    csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
+    x = torch.randn(n, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(5))
+    full = Mixer(csr=csr, device=gpu)
+    perm, bc = full.device_layout()
+    assert bc == 32
+    yb = memory.empty_blocked(n, p, gpu, bc)
+    full.mix_blocked(memory.to_blocked(x, bc), yb, p)
+    y_full = memory.from_blocked(yb, p)
+    covered = 0
+    for r in range(world):
+        sm = StripedMixer(csr, None, world, r, gpu, p)
+        if sm.p_local == 0:
+            continue
+        assert sm.blocked
+        xs = sm.to_layout(x[:, sm.c0:sm.c1].contiguous())
+        ys = sm.empty()
+        sm(xs, ys)
+        assert torch.equal(sm.from_layout(ys), y_full[:, sm.c0:sm.c1]), r
+        covered += sm.p_local
+    assert covered == p
