@@ -148,6 +148,22 @@ def test_tile_lds_bitwise(name, rt, gpu, oracle_mod):
         assert ok, (name, rt, worst)
 
 
+@pytest.mark.parametrize("rt", [8, 16])
+@pytest.mark.parametrize("name", golden_cases())
+def test_tile_lds_bitwise_full_height_tiles(name, rt, gpu, oracle_mod, monkeypatch):
+    """Tiles of RT rows (no unused slot: NIIDMIX_TILE_LDS_PAD=0), so positions every row takes go
+    through the per-position path instead of the branch-free save/restore of the pad slot: still
+    bit-identical to the reference."""
+    monkeypatch.setenv("NIIDMIX_TILE_LDS_PAD", "0")
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    m = _tile_lds_mixer(g, gpu, rt)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-lds-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"]), (name, rt)
+
+
 def test_tile_lds_strided_window(gpu, oracle_mod):
     """A column window of a wider slab (ld > p, p not a multiple of 128 or 4)."""
     g = load_golden("dcliques1000_fc_p64")
