@@ -1,10 +1,10 @@
 #!/usr/bin/env python
 """Exact-mode (bit-identical) round A/B on the headline topology (tuning tool, not the bench): the
-LDS-staged merged-order tile kernel at tile heights --rts, position metadata by scalar loads or
-lane-parallel v_readlane (NIIDMIX_TILE_LDS_META), interleaved in one process; results of every
-variant are checked bitwise against the first.
+LDS-staged merged-order tile kernel at tile heights --rts, interleaved in one process; results of
+every variant are checked bitwise against the first (--no-check for the phase-split builds of
+tools/tlds_split.sh, whose results are not the mix).
 
-    python tools/exact_probe.py [--rts 8,16] [--metas scalar,lanes] [--reps 2]
+    python tools/exact_probe.py [--rts 8,16] [--reps 2] [--order clique|rank]
 """
 import argparse
 import os
@@ -20,7 +20,6 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rts", default="8,16")
-    ap.add_argument("--metas", default="lanes")
     ap.add_argument("--p", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=2)
@@ -52,8 +51,7 @@ def main():
     res = {}
     for rep in range(a.reps):
         for rt, m in mixers.items():
-            for meta in a.metas.split(","):
-                os.environ["NIIDMIX_TILE_LDS_META"] = meta
+            for meta in ("lanes",):
                 m(x, out=y, kernel="tile-lds-exact")
                 torch.cuda.synchronize()
                 if ref is None:
