@@ -138,15 +138,39 @@ def _split(rows, rt):
     return parts
 
 
-def _class_tiles(group, rp, val, rt, max_rows=None):
+def _list_rank(group, rp, col):
+    """{row: median index of the row in the other group rows' in-group edge lists}: the order the
+    group's lists roughly agree on (the reference's set iteration order)."""
+    g = np.asarray(group, np.int64)
+    if len(g) == 0:
+        return {}
+    inside = np.zeros(int(g.max()) + 1, bool)
+    inside[g] = True
+    pos = {int(r): [] for r in g}
+    for r in g:
+        c = col[rp[r] + 1:rp[r + 1]].astype(np.int64)
+        c = c[c < len(inside)]
+        for i, m in enumerate(c[inside[c]].tolist()):
+            pos[m].append(i)
+    return {m: (float(np.median(v)) if v else 0.0) for m, v in pos.items()}
+
+
+def _class_tiles(group, rp, col, val, rt, max_rows=None):
     """Tiles of a row group: rows ordered by degree — under Metropolis-Hastings the weight
     W[j, i] = 1/(max(d_i, d_j) + 1) a source j carries into row i depends on i only through d_i —
     and each degree class cut on its own, so a source's weight is the same across a tile's rows
     (POS_UNIFORM; checked on the actual values) — e.g. the gateway rows of a D-Clique form their own
     tile.  Classes of fewer than max(2, rt/2) rows are merged into a neighbouring class (their
-    positions are then weighted per row)."""
+    positions are then weighted per row).
+
+    Inside a class the rows follow the group's common list order (_list_rank) before the cut.  A
+    tile row skips only its own position, so a tile of rows adjacent in that order has its skips in
+    one run, and every row takes all its other positions (the kernel's cheapest form).  On the
+    1000-node d-cliques topology the share of 4-position groups that every row takes rises from
+    54 % to 77 %.  Results do not change: each row keeps its own list."""
     key = lambda r: int(rp[r + 1] - rp[r])
-    rows = sorted(group, key=key)
+    rank = _list_rank(group, rp, col)
+    rows = sorted(group, key=lambda r: (key(r), rank[int(r)]))
     runs = []
     for r in rows:
         if runs and key(runs[-1][-1]) == key(r):
@@ -188,7 +212,7 @@ def build_tile_plan(csr, groups=None, rt=16, max_rows=None):
     pos_src, pos_mask, pos_w = [], [], []
     grp_tile_ptr = [0]
     for g in groups:
-        for part in _class_tiles(g, rp, val, rt, max_rows):
+        for part in _class_tiles(g, rp, col, val, rt, max_rows):
             lists = [(col[rp[r] + 1:rp[r + 1]], val[rp[r] + 1:rp[r + 1]]) for r in part]
             pad = full & ~((1 << len(part)) - 1)
             for c, mask, ws in _merge(lists):
@@ -260,7 +284,7 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
     # pad slot at positions every row takes (k_mix_tile_lds, "simple" chunks); when that costs more
     # tiles than a group may have, full-height tiles (correct, slower)
     max_rows = rt - 1 if os.environ.get("NIIDMIX_TILE_LDS_PAD", "1") == "1" else rt
-    if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.val, rt, max_rows)) > LDS_MAX_WAVES[rt]
+    if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.col, csr.val, rt, max_rows)) > LDS_MAX_WAVES[rt]
                       for g in groups):
         max_rows = rt
     tp, why = build_tile_plan(csr, groups, rt, max_rows)
@@ -276,7 +300,11 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
         t0, t1 = int(gtp[gi]), int(gtp[gi + 1])
         p0, p1 = int(tp.sub_ptr[t0]), int(tp.sub_ptr[t1])
         rows = tp.sub_rows[t0 * rt:t1 * rt]
-        srcs = np.unique(np.concatenate([tp.pos_src[p0:p1] & row_mask, rows[rows >= 0]]))
+        # slots numbered in list order (first appearance): consecutive positions then mostly read
+        # consecutive slots, which k_mix_tile_lds reads from one address with immediate offsets
+        seq = np.concatenate([tp.pos_src[p0:p1] & row_mask, rows[rows >= 0]])
+        _, first = np.unique(seq, return_index=True)
+        srcs = seq[np.sort(first)]
         if len(srcs) > LDS_MAX_SRC:
             return None, f"group {gi} reads {len(srcs)} distinct rows (> {LDS_MAX_SRC})"
         if t1 - t0 > LDS_MAX_WAVES[rt]:
