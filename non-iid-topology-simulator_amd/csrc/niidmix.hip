@@ -1176,6 +1176,115 @@ struct TileAcc {
 };
 static_assert(sizeof(TileAcc<32>) == 64 * sizeof(float), "two halves of 16 pairs");
 
+// The exact RT = 16 position loop over a run of "easy" positions (uniform weight, taken by every
+// tile row or by all rows but one), hand-scheduled.  Written in C++, the dynamic row index of the
+// skip-one form (s_set_gpr_idx + v_mov) made the compiler keep the 16 accumulator pairs in two
+// register tuples and copy all of them at every merge of the loop's paths (16 v_mov_b64 per group
+// of positions, more on the partial paths) — ~1/3 of the loop's VALU work.  Here the tuple is
+// pinned to v[32:63] for the whole run and every update is in place.
+//   positions j .. stop-1 of the current 64-position chunk (lanes of the descriptor registers):
+//   v_addr  LDS byte address of the position's staged source row (lane j for position j)
+//   v_w     the uniform weight (fp32 bits);  v_skip2  2 * (row that skips it), -1 = every row
+//   lane8   this lane's byte offset in a staged row
+// Per position: fl(w * x) once for the tile (v_pk_mul, the weight broadcast from an SGPR), then one
+// v_pk_add per row in the reference's rounding; a skip-one position saves the skipped row, adds
+// to all and restores it (bit-exact).  The next position's LDS read is in flight while the current
+// one is applied (unrolled by 2: v[64:65] / v[66:67]).  Hazards: an SGPR written by v_readlane is
+// read by a VALU at least 2 wait states later (s_nop 1 or other instructions in between).
+#ifndef NIIDMIX_TLDS_ASM
+#define NIIDMIX_TLDS_ASM 1
+#endif
+#define NIIDMIX_ADD16(T)                                                                            \
+    "v_pk_add_f32 v[32:33], v[32:33], " T "\n\tv_pk_add_f32 v[34:35], v[34:35], " T "\n\t"          \
+    "v_pk_add_f32 v[36:37], v[36:37], " T "\n\tv_pk_add_f32 v[38:39], v[38:39], " T "\n\t"          \
+    "v_pk_add_f32 v[40:41], v[40:41], " T "\n\tv_pk_add_f32 v[42:43], v[42:43], " T "\n\t"          \
+    "v_pk_add_f32 v[44:45], v[44:45], " T "\n\tv_pk_add_f32 v[46:47], v[46:47], " T "\n\t"          \
+    "v_pk_add_f32 v[48:49], v[48:49], " T "\n\tv_pk_add_f32 v[50:51], v[50:51], " T "\n\t"          \
+    "v_pk_add_f32 v[52:53], v[52:53], " T "\n\tv_pk_add_f32 v[54:55], v[54:55], " T "\n\t"          \
+    "v_pk_add_f32 v[56:57], v[56:57], " T "\n\tv_pk_add_f32 v[58:59], v[58:59], " T "\n\t"          \
+    "v_pk_add_f32 v[60:61], v[60:61], " T "\n\tv_pk_add_f32 v[62:63], v[62:63], " T "\n\t"
+// exact: fl(w * x) once for the tile, then one add per row;  fast: one fma per row
+#define NIIDMIX_UPD_EXACT(XD) "v_pk_mul_f32 v[72:73], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("v[72:73]")
+#define NIIDMIX_FMA1(R, XD) "v_pk_fma_f32 " R ", " XD ", s[44:45], " R " op_sel_hi:[1,0,1]\n\t"
+#define NIIDMIX_UPD_FAST(XD)                                                                        \
+    NIIDMIX_FMA1("v[32:33]", XD) NIIDMIX_FMA1("v[34:35]", XD) NIIDMIX_FMA1("v[36:37]", XD)            \
+    NIIDMIX_FMA1("v[38:39]", XD) NIIDMIX_FMA1("v[40:41]", XD) NIIDMIX_FMA1("v[42:43]", XD)            \
+    NIIDMIX_FMA1("v[44:45]", XD) NIIDMIX_FMA1("v[46:47]", XD) NIIDMIX_FMA1("v[48:49]", XD)            \
+    NIIDMIX_FMA1("v[50:51]", XD) NIIDMIX_FMA1("v[52:53]", XD) NIIDMIX_FMA1("v[54:55]", XD)            \
+    NIIDMIX_FMA1("v[56:57]", XD) NIIDMIX_FMA1("v[58:59]", XD) NIIDMIX_FMA1("v[60:61]", XD)            \
+    NIIDMIX_FMA1("v[62:63]", XD)
+// one position k of the 4-way unrolled loop: data in XD (read two positions ago), its descriptor
+// in SM; the read of position j+2 goes into XP with its descriptor into SP.  A skip-one position
+// branches to an out-of-line block (SKIPBLK), so the common full position falls through.
+#define NIIDMIX_TLDS_POS(XD, SM, XP, SP, K, UPD)                                                    \
+    "s_add_u32 s47, %[j], 2\n\t"                                                                    \
+    "s_min_u32 s47, s47, %[last]\n\t"                                                               \
+    "v_readlane_b32 " SP ", %[vm], s47\n\t"                                                         \
+    "v_readlane_b32 s44, %[vw], %[j]\n\t"                                                           \
+    "s_and_b32 s46, " SP ", 0xffffff\n\t"                                                           \
+    "v_add_u32 v76, s46, %[l8]\n\t"                                                                 \
+    "ds_read_b64 " XP ", v76\n\t"                                                                   \
+    "s_lshr_b32 s46, " SM ", 24\n\t"                                                                \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                      \
+    "s_cmp_lg_u32 s46, 0\n\t"                                                                       \
+    "s_cbranch_scc1 .Ltlds_skip" K "_%=\n\t" UPD(XD)                                                \
+    "\n.Ltlds_back" K "_%=:\n\t"                                                                    \
+    "s_add_u32 %[j], %[j], 1\n\t"                                                                   \
+    "s_cmp_ge_u32 %[j], %[stop]\n\t"                                                                \
+    "s_cbranch_scc1 .Ltlds_done_%=\n\t"
+#define NIIDMIX_TLDS_SKIPBLK(XD, K, UPD)                                                            \
+    "\n.Ltlds_skip" K "_%=:\n\t"                                                                    \
+    "s_sub_u32 s46, s46, 2\n\t"                                                                     \
+    "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
+    "v_mov_b32 v74, v32\n\t"                                                                        \
+    "v_mov_b32 v75, v33\n\t"                                                                        \
+    "s_set_gpr_idx_off\n\t" UPD(XD)                                                                 \
+    "s_set_gpr_idx_on s46, gpr_idx(DST)\n\t"                                                        \
+    "v_mov_b32 v32, v74\n\t"                                                                        \
+    "v_mov_b32 v33, v75\n\t"                                                                        \
+    "s_set_gpr_idx_off\n\t"                                                                         \
+    "s_branch .Ltlds_back" K "_%=\n\t"
+// descriptor of a position: LDS byte address of its staged row | (2 * skipped row + 2) << 24 (0:
+// every row takes it)
+#define NIIDMIX_TLDS_RUN(UPD)                                                                       \
+    asm volatile("s_mov_b32 s47, %[j]\n\t"                                                          \
+                 "v_readlane_b32 s40, %[vm], s47\n\t"                                               \
+                 "s_add_u32 s47, %[j], 1\n\t"                                                       \
+                 "s_min_u32 s47, s47, %[last]\n\t"                                                  \
+                 "v_readlane_b32 s41, %[vm], s47\n\t"                                               \
+                 "s_and_b32 s46, s40, 0xffffff\n\t"                                                 \
+                 "v_add_u32 v76, s46, %[l8]\n\t"                                                    \
+                 "ds_read_b64 v[64:65], v76\n\t"                                                    \
+                 "s_and_b32 s46, s41, 0xffffff\n\t"                                                 \
+                 "v_add_u32 v76, s46, %[l8]\n\t"                                                    \
+                 "ds_read_b64 v[66:67], v76\n"                                                      \
+                 ".Ltlds_loop_%=:\n\t"                                                              \
+                 NIIDMIX_TLDS_POS("v[64:65]", "s40", "v[68:69]", "s42", "0", UPD)                  \
+                 NIIDMIX_TLDS_POS("v[66:67]", "s41", "v[70:71]", "s43", "1", UPD)                  \
+                 NIIDMIX_TLDS_POS("v[68:69]", "s42", "v[64:65]", "s40", "2", UPD)                  \
+                 NIIDMIX_TLDS_POS("v[70:71]", "s43", "v[66:67]", "s41", "3", UPD)                  \
+                 "s_branch .Ltlds_loop_%=\n\t"                                                      \
+                 NIIDMIX_TLDS_SKIPBLK("v[64:65]", "0", UPD)                                         \
+                 NIIDMIX_TLDS_SKIPBLK("v[66:67]", "1", UPD)                                         \
+                 NIIDMIX_TLDS_SKIPBLK("v[68:69]", "2", UPD)                                         \
+                 NIIDMIX_TLDS_SKIPBLK("v[70:71]", "3", UPD)                                         \
+                 "\n.Ltlds_done_%=:\n\t"                                                            \
+                 "s_waitcnt lgkmcnt(0)"                                                             \
+                 : "+{v[32:63]}"(acc), [j] "+s"(j)                                                  \
+                 : [stop] "s"(stop), [last] "s"(last), [vm] "v"(v_meta), [vw] "v"(v_w),             \
+                   [l8] "v"(lane8)                                                                  \
+                 : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74",     \
+                   "v75", "v76", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "scc",     \
+                   "memory")
+typedef TileAcc<16>::V Acc16;
+template <bool EXACT>
+__device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_meta, int v_w,
+                                           int lane8) {
+    const int last = stop - 1;
+    if constexpr (EXACT) NIIDMIX_TLDS_RUN(NIIDMIX_UPD_EXACT);
+    else NIIDMIX_TLDS_RUN(NIIDMIX_UPD_FAST);
+}
+
 // Apply op(acc_row, r) to the rows of the wave-uniform mask m.  No per-row select: on gfx950 a lane
 // mask or SGPR operand that a SALU op just wrote stalls the VALU ~30-40 cycles per row
 // (tools/valu_probe.hip: the select form of a partial position cost ~10x a full one).  Instead,
@@ -1271,6 +1380,9 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int64_t col = c0 + 2 * lane;
     const bool ok = col < p;                     // p even: a lane's pair is all-in or all-out
     const int tb = grp_tile_ptr[grp], te = grp_tile_ptr[grp + 1];
+    typedef __attribute__((address_space(3))) float lds_float;
+    const unsigned lds_base = (unsigned)(size_t)(lds_float *)lds_tile;   // LDS byte offset of stage
+    const int lane8 = lane * (int)sizeof(f2);
     for (int sub = tb + wave; sub < te; sub += n_waves) {
         const int li = lane < RT ? lane : RT - 1;
         const int d_row = sub_rows[sub * RT + li];
@@ -1303,6 +1415,37 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             // tiles (two register halves make the dynamic row index a branch) test each position.
             const uint32_t miss = ~(uint32_t)d_mask & FULL;
             const bool simple = (d_src & kPosUniform) != 0 && (miss & (miss - 1u)) == 0u && (miss != 0u || pad_slot);
+            if constexpr (RT == 16 && NIIDMIX_TLDS_ASM && NIIDMIX_TLDS_SPLIT == 0) {
+                // Runs of positions with a uniform weight that every row or all rows but one take
+                // go through tlds16_run (hand-scheduled, accumulators in place); any other
+                // position (rare) through the per-row form.
+                const bool easy = (d_src & kPosUniform) != 0 && (miss & (miss - 1u)) == 0u;
+                const uint64_t hard_bits = __ballot(lane < cnt && !easy);
+                const int v_meta = ((d_src & kPosRowMask) * (64 * (int)sizeof(f2)) + (int)lds_base) |
+                                   (miss ? (2 * __builtin_ctz(miss) + 2) << 24 : 0);
+                int j = 0;
+                while (j < cnt) {
+                    const uint64_t rest = hard_bits >> j;                // j < 64
+                    const int stop = rest ? j + __builtin_ctzll(rest) : cnt;
+                    if (stop > j) {
+                        tlds16_run<EXACT>(acc.v[0], j, stop, v_meta, d_wu, lane8);
+                        j = stop;
+                    }
+                    if (j < cnt) {                                       // one hard position
+                        const int sj = __builtin_amdgcn_readlane(d_src, j);
+                        const f2 xu = stage[(sj & kPosRowMask) * 64 + lane];
+                        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j) & FULL;
+                        const float wu = __int_as_float(__builtin_amdgcn_readlane(d_wu, j));
+                        const float *wp = pos_w + (kb + j) * RT;
+                        for (uint32_t b = m; b; b &= b - 1u) {
+                            const int r = __builtin_ctz(b);
+                            acc.set(r, axpy2<EXACT>((sj & kPosUniform) ? wu : wp[r], xu, acc.get(r)));
+                        }
+                        ++j;
+                    }
+                }
+                continue;
+            }
             if (RT <= 16 && NIIDMIX_TLDS_SPLIT == 0) {
                 const int d_skip = miss ? __builtin_ctz(miss) : RT - 1;
                 // SIMPLE position: save the skipped row, update all rows in place, restore it

@@ -280,10 +280,12 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
             n_src = len(np.unique(np.concatenate([col[idx], g])))
             if n_src > LDS_MAX_SRC:
                 return None, f"group {gi} reads {n_src} distinct rows (> {LDS_MAX_SRC})"
-    # tiles of at most rt-1 rows leave slot rt-1 unused: the kernel's branch-free loop skips that
-    # pad slot at positions every row takes (k_mix_tile_lds, "simple" chunks); when that costs more
-    # tiles than a group may have, full-height tiles (correct, slower)
-    max_rows = rt - 1 if os.environ.get("NIIDMIX_TILE_LDS_PAD", "1") == "1" else rt
+    # tiles of at most rt-1 rows leave slot rt-1 unused: the rt 8 / 32 loops skip that pad slot at
+    # positions every row takes (k_mix_tile_lds, "simple" chunks); when that costs more tiles than
+    # a group may have, full-height tiles (correct, slower).  The rt 16 loop (tlds16_run) needs no
+    # pad: full-height tiles, one tile fewer per 1000-node d-clique (7 instead of 8).
+    pad_default = "0" if rt == 16 else "1"
+    max_rows = rt - 1 if os.environ.get("NIIDMIX_TILE_LDS_PAD", pad_default) == "1" else rt
     if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.col, csr.val, rt, max_rows)) > LDS_MAX_WAVES[rt]
                       for g in groups):
         max_rows = rt
