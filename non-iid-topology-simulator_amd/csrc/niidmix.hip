@@ -1325,7 +1325,7 @@ __device__ __forceinline__ void apply_mask(TileAcc<RT> &acc, uint32_t m, Op op) 
 #endif
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
-template <bool EXACT, int RT, int SV>
+template <bool EXACT, int RT, int SV, int RS>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
@@ -1333,7 +1333,10 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
-    constexpr int64_t CW = 128;                  // columns per item: 64 lanes x 2
+    // RS = column pairs per item and staged row: 64 (all lanes), or 60 so that a third block fits a
+    // CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
+    constexpr int rs = RS;
+    constexpr int64_t CW = 2 * RS;               // columns per item
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                         // positions read together
     extern __shared__ float lds_tile[];          // [n_src][64] column pairs
@@ -1378,7 +1381,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     }
     __syncthreads();
     const int64_t col = c0 + 2 * lane;
-    const bool ok = col < p;                     // p even: a lane's pair is all-in or all-out
+    const bool ok = lane < rs && col < p;        // p even: a lane's pair is all-in or all-out
     const int tb = grp_tile_ptr[grp], te = grp_tile_ptr[grp + 1];
     typedef __attribute__((address_space(3))) float lds_float;
     const unsigned lds_base = (unsigned)(size_t)(lds_float *)lds_tile;   // LDS byte offset of stage
@@ -1391,7 +1394,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         TileAcc<RT> acc;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
-            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
+            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + lane];
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
             acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
         }
@@ -1421,7 +1424,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 // position (rare) through the per-row form.
                 const bool easy = (d_src & kPosUniform) != 0 && (miss & (miss - 1u)) == 0u;
                 const uint64_t hard_bits = __ballot(lane < cnt && !easy);
-                const int v_meta = ((d_src & kPosRowMask) * (64 * (int)sizeof(f2)) + (int)lds_base) |
+                const int v_meta = ((d_src & kPosRowMask) * (rs * (int)sizeof(f2)) + (int)lds_base) |
                                    (miss ? (2 * __builtin_ctz(miss) + 2) << 24 : 0);
                 int j = 0;
                 while (j < cnt) {
@@ -1433,7 +1436,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     }
                     if (j < cnt) {                                       // one hard position
                         const int sj = __builtin_amdgcn_readlane(d_src, j);
-                        const f2 xu = stage[(sj & kPosRowMask) * 64 + lane];
+                        const f2 xu = stage[(sj & kPosRowMask) * rs + lane];
                         const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j) & FULL;
                         const float wu = __int_as_float(__builtin_amdgcn_readlane(d_wu, j));
                         const float *wp = pos_w + (kb + j) * RT;
@@ -1489,7 +1492,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 // (A third form for all-simple groups measured the same: 4.80 vs 4.79 ms.)
                 const uint64_t slow_bits = __ballot(lane < cnt && !simple);
                 const uint64_t part_bits = slow_bits | __ballot(lane < cnt && miss != 0u);
-                const int d_addr = (d_src & kPosRowMask) * 64;   // LDS f2 index of each position
+                const int d_addr = (d_src & kPosRowMask) * rs;   // LDS f2 index of each position
                 const int nd = cnt & ~(D - 1);
                 f2 xa[D], xb[D];
 #pragma unroll
@@ -1528,12 +1531,12 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             f2 xa[D], xb[D];
 #pragma unroll
             for (int u = 0; u < D; ++u)
-                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * 64 + lane];
+                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * rs + lane];
             for (int j = 0; j < cnt; j += D) {
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     const int jn = j + D + u < cnt ? j + D + u : cnt - 1;
-                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * 64 + lane];
+                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * rs + lane];
                 }
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
@@ -1575,7 +1578,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             if (row < 0) continue;                                  // wave-uniform
             f2 o = acc.get(r);
             if (!avg_only) {
-                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * 64 + lane];
+                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + lane];
                 o = xs * 0.f + o;
             }
             if (ok) {
@@ -2201,13 +2204,26 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         return set_error(NIIDMIX_EUNSUPPORTED, "LDS tile kernel needs even p, ld and 8-B aligned slabs");
     const int sv = (p % 4 == 0 && ld_x % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 4 : 2;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int64_t n_chunks = (p + 127) / 128;
+    // Item width: 128 columns, or - rt 16 - 120 when that lets THREE blocks share a CU's 160 KB
+    // of LDS and 128 allows only two (1000-node d-cliques: 109 staged rows, 52 KB per block).  The
+    // position loop is latency-bound, so the third block's waves are worth 4 idle lanes (same box:
+    // 3.85 vs 4.07 ms; one block per CU 7.3 ms).  124 and 112 columns measured slower than 120.
+    int cw = 128;
+    const size_t lds_cu = 160 * 1024;
+    if (plan->rt == 16 && (size_t)plan->max_src * 128 * sizeof(float) > lds_cu / 3 &&
+        (size_t)plan->max_src * 120 * sizeof(float) <= lds_cu / 3)
+        cw = 120;
+    if (const char *e = getenv("NIIDMIX_TLDS_COLS")) {          // tuning override: 128 or 120
+        const int v = atoi(e);
+        if (v == 128 || v == 120) cw = v;
+    }
+    const int64_t n_chunks = (p + cw - 1) / cw;
     const int64_t n_items = (int64_t)plan->n_grp * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
-    const size_t lds = (size_t)plan->max_src * 128 * sizeof(float);
+    const size_t lds = (size_t)plan->max_src * cw * sizeof(float);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = k_mix_tile_lds<E, R, V>; \
+        auto kfn = cw == 120 ? k_mix_tile_lds<E, R, V, 60> : k_mix_tile_lds<E, R, V, 64>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
         hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \

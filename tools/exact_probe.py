@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--order", default="clique", choices=["rank", "clique"])
     ap.add_argument("--no-check", action="store_true", help="phase-split builds: results are not the mix")
+    ap.add_argument("--lds-rows", type=int, default=0,
+                    help="occupancy probe: reserve LDS for this many staged rows (max_src) per block")
     a = ap.parse_args()
     from niidmix import memory, ops
     dev = torch.device("cuda:0")
@@ -42,6 +44,8 @@ def main():
         os.environ["NIIDMIX_TILE_LDS_RT"] = rt
         m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
         assert m.tlds is not None, m.tlds_reason
+        if a.lds_rows:
+            m.tlds.max_src = max(m.tlds.max_src, a.lds_rows)
         mixers[int(rt)] = m
     n = csr.n
     x = memory.empty_slab(n, a.p, dev)
