@@ -123,3 +123,31 @@ def test_uniform_positions_dominate_dcliques():
     tp, _ = tile.build_tile_plan(csr, g["cliques"], 16)
     frac = np.mean((tp.pos_src & tile.POS_UNIFORM) != 0)
     assert frac > 0.95, frac
+
+
+def test_lds_plan_runs_dcliques():
+    """rt-16 LDS plan on the headline topology: full-height tiles (7 per clique, no pad slot),
+    rows in the clique's list order so that most 4-position groups are taken by every row, and
+    slots numbered in list order so that most consecutive positions read consecutive slots."""
+    from niidmix import tile
+    g = load_golden("dcliques1000_fc_p64")
+    csr = _csr(g).validate()
+    lp, why = tile.build_tile_lds_plan(csr, g["cliques"], 16)
+    assert lp is not None, why
+    tp = lp.tile
+    assert lp.max_tiles == 7 and tp.n_sub == 70
+    full = (1 << 16) - 1
+    groups = every_row = consecutive = pairs = 0
+    for t in range(tp.n_sub):
+        b, e = int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])
+        n = int(np.sum(tp.sub_rows[t * 16:(t + 1) * 16] >= 0))
+        rows = (1 << n) - 1
+        taken = [(int(tp.pos_mask[k]) & rows) == rows for k in range(b, e)]
+        for j in range(0, (e - b) & ~3, 4):
+            groups += 1
+            every_row += all(taken[j:j + 4])
+        slots = lp.pos_slot[b:e] & (tile.POS_UNIFORM - 1)
+        consecutive += int(np.sum(np.diff(slots) == 1))
+        pairs += len(slots) - 1
+    assert every_row / groups > 0.7, every_row / groups
+    assert consecutive / pairs > 0.8, consecutive / pairs
