@@ -151,9 +151,9 @@ def test_tile_lds_bitwise(name, rt, gpu, oracle_mod):
 @pytest.mark.parametrize("rt", [8, 16])
 @pytest.mark.parametrize("name", golden_cases())
 def test_tile_lds_bitwise_full_height_tiles(name, rt, gpu, oracle_mod, monkeypatch):
-    """Tiles of RT rows (no unused slot: NIIDMIX_TILE_LDS_PAD=0), so positions every row takes go
-    through the per-position path instead of the branch-free save/restore of the pad slot: still
-    bit-identical to the reference."""
+    """Tiles of RT rows (no unused slot: NIIDMIX_TILE_LDS_PAD=0; the rt-16 default, whose
+    hand-scheduled loop needs no pad), so rt 8's positions every row takes go through the
+    per-position path instead of the save/restore of the pad slot: still bit-identical."""
     monkeypatch.setenv("NIIDMIX_TILE_LDS_PAD", "0")
     g = load_golden(name)
     if g["x"].shape[1] % 2:
@@ -162,6 +162,34 @@ def test_tile_lds_bitwise_full_height_tiles(name, rt, gpu, oracle_mod, monkeypat
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel="tile-lds-exact").cpu().numpy()
     assert oracle_mod.bitwise_equal(y, g["y"]), (name, rt)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_tile_lds_narrow_items_bitwise(name, gpu, oracle_mod, monkeypatch):
+    """120-column items (the launcher's choice when that lets a third block share a CU; forced
+    here by NIIDMIX_TLDS_COLS) are bit-identical on every golden case with even p."""
+    monkeypatch.setenv("NIIDMIX_TLDS_COLS", "120")
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    m = _tile_lds_mixer(g, gpu, 16)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-lds-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"]), name
+
+
+def test_tile_lds_narrow_items_float2(gpu, oracle_mod):
+    """The 1000-node d-cliques plan picks 120-column items by itself (109 staged rows); p = 1002
+    (p % 4 == 2: float2 staging) ends in a ragged item.  Bitwise against the C oracle."""
+    g = load_golden("dcliques1000_fc_p64")
+    x = np.random.default_rng(5).standard_normal((g["x"].shape[0], 1002)).astype(np.float32)
+    x[3, 7] = -0.0
+    x[11, 1001] = np.float32(1e-42)
+    m = _tile_lds_mixer(g, gpu, 16)
+    assert m.tlds.max_src * 128 * 4 > 160 * 1024 // 3 >= m.tlds.max_src * 120 * 4
+    y = m(torch.from_numpy(x).to(gpu), kernel="tile-lds-exact").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(x, g["row_ptr"], g["col"], g["val"])
+    assert oracle_mod.bitwise_equal(y, ref)
 
 
 def test_tile_lds_strided_window(gpu, oracle_mod):
