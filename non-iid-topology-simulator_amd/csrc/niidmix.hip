@@ -1333,8 +1333,8 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
-    // RS = column pairs per item and staged row: 64 (all lanes), or 60 so that a third block fits a
-    // CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
+    // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
+    // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
     constexpr int64_t CW = 2 * RS;               // columns per item
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
@@ -2204,18 +2204,27 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         return set_error(NIIDMIX_EUNSUPPORTED, "LDS tile kernel needs even p, ld and 8-B aligned slabs");
     const int sv = (p % 4 == 0 && ld_x % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 4 : 2;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // Item width: 128 columns, or - rt 16 - 120 when that lets THREE blocks share a CU's 160 KB
-    // of LDS and 128 allows only two (1000-node d-cliques: 109 staged rows, 52 KB per block).  The
-    // position loop is latency-bound, so the third block's waves are worth 4 idle lanes (same box:
-    // 3.85 vs 4.07 ms; one block per CU 7.3 ms).  124 and 112 columns measured slower than 120.
+    // Item width (rt 16): the widest of 128, 120 and 96 columns that fits the most blocks per CU in
+    // its 160 KB of LDS, up to three (three 7-wave blocks fill the 6 waves per SIMD the kernel's 80
+    // VGPRs allow).  The position loop is latency-bound, so another block's waves are worth idle
+    // lanes.  1000-node d-cliques: 109 staged rows -> 120 columns, three blocks (same box 3.85 vs
+    // 4.07 ms at 128; one block per CU 7.3 ms); 10 000 nodes: 199 rows -> 96 columns, two blocks
+    // instead of one.  124 and 112 columns measured slower than 120.
     int cw = 128;
     const size_t lds_cu = 160 * 1024;
-    if (plan->rt == 16 && (size_t)plan->max_src * 128 * sizeof(float) > lds_cu / 3 &&
-        (size_t)plan->max_src * 120 * sizeof(float) <= lds_cu / 3)
-        cw = 120;
-    if (const char *e = getenv("NIIDMIX_TLDS_COLS")) {          // tuning override: 128 or 120
+    if (plan->rt == 16) {
+        auto blocks = [&](int c) {
+            const size_t per = (size_t)plan->max_src * c * sizeof(float);
+            const size_t b = per ? lds_cu / per : 3;
+            return (int)(b < 3 ? b : 3);
+        };
+        const int target = blocks(96);
+        for (int c : {128, 120, 96})
+            if (blocks(c) >= target) { cw = c; break; }
+    }
+    if (const char *e = getenv("NIIDMIX_TLDS_COLS")) {          // tuning override: 128, 120 or 96
         const int v = atoi(e);
-        if (v == 128 || v == 120) cw = v;
+        if (v == 128 || v == 120 || v == 96) cw = v;
     }
     const int64_t n_chunks = (p + cw - 1) / cw;
     const int64_t n_items = (int64_t)plan->n_grp * ((n_chunks + 7) / 8) * 8;
@@ -2223,7 +2232,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const size_t lds = (size_t)plan->max_src * cw * sizeof(float);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = cw == 120 ? k_mix_tile_lds<E, R, V, 60> : k_mix_tile_lds<E, R, V, 64>; \
+        auto kfn = cw == 120 ? k_mix_tile_lds<E, R, V, 60> : cw == 96 ? k_mix_tile_lds<E, R, V, 48> : k_mix_tile_lds<E, R, V, 64>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
         hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \

@@ -164,18 +164,19 @@ def test_tile_lds_bitwise_full_height_tiles(name, rt, gpu, oracle_mod, monkeypat
     assert oracle_mod.bitwise_equal(y, g["y"]), (name, rt)
 
 
+@pytest.mark.parametrize("cols", ["120", "96"])
 @pytest.mark.parametrize("name", golden_cases())
-def test_tile_lds_narrow_items_bitwise(name, gpu, oracle_mod, monkeypatch):
-    """120-column items (the launcher's choice when that lets a third block share a CU; forced
-    here by NIIDMIX_TLDS_COLS) are bit-identical on every golden case with even p."""
-    monkeypatch.setenv("NIIDMIX_TLDS_COLS", "120")
+def test_tile_lds_narrow_items_bitwise(name, cols, gpu, oracle_mod, monkeypatch):
+    """120- and 96-column items (the launcher's choice when that lets another block share a CU;
+    forced here by NIIDMIX_TLDS_COLS) are bit-identical on every golden case with even p."""
+    monkeypatch.setenv("NIIDMIX_TLDS_COLS", cols)
     g = load_golden(name)
     if g["x"].shape[1] % 2:
         pytest.skip("odd p: the LDS tile kernel reads column pairs")
     m = _tile_lds_mixer(g, gpu, 16)
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel="tile-lds-exact").cpu().numpy()
-    assert oracle_mod.bitwise_equal(y, g["y"]), name
+    assert oracle_mod.bitwise_equal(y, g["y"]), (name, cols)
 
 
 def test_tile_lds_narrow_items_float2(gpu, oracle_mod):
