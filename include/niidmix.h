@@ -19,7 +19,10 @@
  * Slabs are row-major fp32 [rows, p] with leading dimension ld (elements).  One row = the flattened
  * parameters of one simulated node in model.parameters() order.
  * Jacobi semantics: every output row is computed from the pre-round input, so x and y must not
- * overlap (checked: NIIDMIX_EALIAS).
+ * overlap (checked: NIIDMIX_EALIAS).  Entry points that get the row count as an argument check the
+ * full [rows, ld] extents; the tile entry points (niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32)
+ * keep their row lists in device memory and can only reject x == y, so the caller (niidmix.ops,
+ * which owns both slabs) guarantees that partly overlapping slabs are never passed there.
  */
 #ifndef NIIDMIX_H
 #define NIIDMIX_H

@@ -157,7 +157,10 @@ def mix_clique_blocked(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: to
     k, rows, b = x.shape
     _req(0 <= p <= k * b and (k == 0 or p > (k - 1) * b), f"p={p} does not fit {k} blocks of {b}")
     _req(member_row.device == x.device, "plan and slabs must be on the same device")
-    _req(x.data_ptr() != out.data_ptr(), "x and out overlap: mixing is out-of-place")
+    if x.numel() and x.untyped_storage().data_ptr() == out.untyped_storage().data_ptr():
+        ext = ((k - 1) * x.stride(0) + (rows - 1) * x.stride(1) + b) * 4
+        x0, o0 = x.data_ptr(), out.data_ptr()
+        _req(x0 + ext <= o0 or o0 + ext <= x0, "x and out overlap: mixing is out-of-place")
     plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
                           res_member, row_ptr, col, val, max_clique, max_clique_res)
     rc = _lib.lib.niidmix_mix_clique_blocked_f32(x.data_ptr(), out.data_ptr(), int(p), x.stride(1),

@@ -433,3 +433,10 @@ def test_bigclique_blocked_layout(n, size, inter, gpu):
         yb = memory.empty_blocked(n, p, gpu, bc)
         m.mix_blocked(xb, yb, p)
         assert torch.equal(memory.from_blocked(yb, p), y)
+    # partly overlapping blocked slabs in one allocation are refused (Jacobi, d_sgd.py:99-116)
+    k, rows, b = yb.shape
+    flat = torch.zeros(2 * k * rows * b, device=gpu)
+    xo = flat[: k * rows * b].view(k, rows, b)
+    oo = flat[k * rows * b // 2: k * rows * b // 2 + k * rows * b].view(k, rows, b)
+    with pytest.raises(RuntimeError, match="overlap"):
+        m.mix_blocked(xo, oo, p)
