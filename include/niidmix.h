@@ -19,10 +19,13 @@
  * Slabs are row-major fp32 [rows, p] with leading dimension ld (elements).  One row = the flattened
  * parameters of one simulated node in model.parameters() order.
  * Jacobi semantics: every output row is computed from the pre-round input, so x and y must not
- * overlap (checked: NIIDMIX_EALIAS).  Entry points that get the row count as an argument check the
- * full [rows, ld] extents; the tile entry points (niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32)
- * keep their row lists in device memory and can only reject x == y, so the caller (niidmix.ops,
- * which owns both slabs) guarantees that partly overlapping slabs are never passed there.
+ * overlap.  Every entry point that reads one slab and writes another gets the row count and checks
+ * the full extents of both (NIIDMIX_EALIAS), each slab with its own strides.
+ *
+ * ABI 3 (this header): n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
+ * niidmix_grad_segment_mean_f32 and niidmix_grad_segment_mean_blocked_f32 (full extent checks);
+ * niidmix_update_rows_f32 added (the 'sample' topology's broadcast); cliques of <= 112 members
+ * accept 64-column blocks (the multi-clique tile).
  */
 #ifndef NIIDMIX_H
 #define NIIDMIX_H
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define NIIDMIX_ABI_VERSION 2
+#define NIIDMIX_ABI_VERSION 3
 
 enum niidmix_status {
     NIIDMIX_OK = 0,
@@ -156,8 +159,10 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
  * (K = ceil(p / block_cols) blocks of row-major [rows, block_cols] sub-slabs with row stride `ld`
  * floats and block strides block_stride_x / block_stride_y floats), element (r, c) at
  *   base + (c / block_cols) * block_stride + r * ld + c % block_cols.
- * block_cols: a power of two >= 256 (the register tile's 256-column chunks), >= 32 when
- * max_clique > 256 (the big-clique kernel's 32-column items).  This is the layout niidmix keeps
+ * block_cols: a power of two >= 256 (the register tile's 256-column chunks), >= 64 when
+ * max_clique <= 112 (the multi-clique tile's 64-column items, which also serves every plan with
+ * >= 4096 member rows: Q = 4 cliques per item keep a column chunk's rows in an XCD's L2), >= 32
+ * when max_clique > 256 (the big-clique kernel's 32-column items).  This is the layout niidmix keeps
  * device-resident node state in (Mixer.device_layout: block_cols = 1024 for cliques of <= 256
  * members, 256 when a clique has > 64 gateway terms, 32 for big cliques; clique-contiguous rows),
  * which measured robust to the slab's physical placement.  Cliques of <= 256 members use
@@ -198,8 +203,8 @@ typedef struct niidmix_tile_plan {
     const float *pos_w;
 } niidmix_tile_plan;
 
-int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                         const niidmix_tile_plan *plan, int mode, void *stream);
+int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                         int64_t p, const niidmix_tile_plan *plan, int mode, void *stream);
 
 /* LDS-staged merged-order row tiles (exact-mode default for clique topologies): the same tiles and
  * results as niidmix_mix_tile_f32 (bit for bit in NIIDMIX_MODE_EXACT), grouped: a group (a clique)
@@ -230,8 +235,8 @@ typedef struct niidmix_tile_lds_plan {
     const int32_t *grp_src_rows;
 } niidmix_tile_lds_plan;
 
-int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                             const niidmix_tile_lds_plan *plan, int mode, void *stream);
+int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                             int64_t p, const niidmix_tile_lds_plan *plan, int mode, void *stream);
 
 /* Dense mixing Y = W^T X on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), for topologies dense
  * enough that W x Theta is a genuine GEMM (fully-connected, tools/setup/topology/fully-connected.py).
@@ -259,16 +264,16 @@ int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
  *   acc = +0; acc = fl(acc + g_m) in member order; y_m = fl(+0 + fl(acc / len))
  * = average_gradients (d_sgd.py:19-27) + update_gradients (d_sgd.py:37-45), bit for bit.  One read
  * of every member row and one write (HBM-bound), instead of len gathers per output row.
- *   g  [*, ld_g] gradient slab (device), y [*, ld_y] output (device, must not overlap g)
+ *   g  [n_rows, ld_g] gradient slab (device), y [n_rows, ld_y] output (device, must not overlap g)
  *   seg_ptr [n_seg+1], seg_row [seg_ptr[n_seg]] int32 (device).  Rows in no segment are untouched. */
-int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t p,
-                                  int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
-                                  void *stream);
+int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y,
+                                  int64_t n_rows, int64_t p, int64_t n_seg, const int32_t *seg_ptr,
+                                  const int32_t *seg_row, void *stream);
 
 /* niidmix_grad_segment_mean_f32 on column-blocked slabs [K][rows][block_cols] (see
  * niidmix_mix_clique_blocked_f32; block_cols a power of two >= 1024, p % 4 == 0). */
-int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t p, int64_t ld,
-                                          int64_t block_cols, int64_t block_stride_g,
+int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t n_rows, int64_t p,
+                                          int64_t ld, int64_t block_cols, int64_t block_stride_g,
                                           int64_t block_stride_y, int64_t n_seg,
                                           const int32_t *seg_ptr, const int32_t *seg_row,
                                           void *stream);
@@ -282,6 +287,14 @@ int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t p, i
  *   rows [n_rows] int32 rows to step (device) */
 int niidmix_sgd_step_rows_f32(float *p, int64_t ld_p, const float *g, int64_t ld_g, int64_t ncols,
                               const int32_t *rows, int64_t n_rows, float neg_lr, void *stream);
+
+/* update_models(all_models, avg) after the 'sample' topology's uniform average (d_sgd.py:240-250,
+ * :29-35): every row y_i := fl(fl(x_i * 0) + avg) (p.mul_(0.); p.add_(new)) — avg everywhere
+ * except NaN where x_i is non-finite and the sign rule of (+-0) + (+-0) where avg is 0.
+ *   x [n_rows, ld_x], y [n_rows, ld_y] (device; y == x with ld_y == ld_x: in place, any other
+ *   overlap is refused);  avg [p] (device, overlapping neither) */
+int niidmix_update_rows_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                            int64_t p, const float *avg, void *stream);
 
 /* Device memory for node-state slabs, with the signatures of a PyTorch pluggable allocator
  * (torch.cuda.memory.CUDAPluggableAllocator; niidmix.memory.slab_pool uses them for a MemPool).

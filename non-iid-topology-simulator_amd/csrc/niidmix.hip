@@ -107,8 +107,13 @@ __device__ __forceinline__ float4 axpy4(float w, float4 xv, float4 acc) {
 // finite.  Hence every output the fast kernel finds non-finite is recomputed from the node's CSR
 // row in the reference's operand order with fast-mode arithmetic (z = x_self*0, acc = fma(w, x_j,
 // acc), y = z + acc: k_mix_csr's fast mode), which reproduces the reference's inf / NaN pattern.
-// Finite outputs are untouched; the check costs one v_cmp_class per output element.
-//   row-uniform form (one wave, V columns per lane): csr_refix;  per-lane form: csr_refix1.
+// The check costs one v_cmp_class per output element.  What is recomputed: k_mix_clique recomputes
+// every column of a row's chunk once any lane of it is non-finite (its finite neighbours then take
+// the CSR form's bits, still within the tolerance); the multi-clique, big-clique and GEMM kernels
+// recompute only the non-finite elements, each by an O(degree) CSR walk.  A round whose models
+// have diverged to inf / NaN is therefore much slower than a finite one (every element recomputed
+// serially); finite rounds never enter this path.
+//   one row per call, V columns per lane: csr_refix;  one column: csr_refix1.
 template <int V>
 __device__ __forceinline__ void csr_refix(const float *__restrict__ xc, int64_t ld_x, unsigned lo, bool act,
                                        int64_t row, const int64_t *__restrict__ rp,
@@ -573,6 +578,217 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         float o[V];
         csr_refix<V>(xc, ld_x, lo, act, row, csr_ptr, csr_col, csr_val, o);
         if (act) stv_nt<V>(yc + row * ld_y + lo, o);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Multi-clique register tile for topologies with MANY cliques (10 000-node d-cliques: 100 cliques,
+// each gathering one gateway row from every other clique, interclique.py:57-75).  k_mix_clique's
+// item is one clique x 256 columns, so the rows one column chunk needs are N x 1 KB (10 MB at 10 000
+// nodes): more than an XCD's 4 MB L2, and ~73 % of the gateway gathers (one per member) missed it.
+// Here an item is Q cliques x 64 columns: lane quarter q = lane / (64 / Q) works on clique cg*Q + q,
+// 4 columns per lane, so one wave-instruction loads a 256-B piece of Q rows of Q cliques.  Per item
+// the bytes (and registers) are those of k_mix_clique's, but a column chunk's working set is N x 256
+// B (2.5 MB at 10 000 nodes), and the chunk's items run together on one XCD (XCD-aware order), so a
+// gateway row is in that XCD's L2 when its other reader comes for it.
+//   descriptors: lane d < Q*RPW holds (clique d / RPW, slot d % RPW)'s member row, group, coefficients
+//     and first residual entry; lanes fetch theirs with ds_bpermute (__shfl) when they use them;
+//   1. member rows -> registers (RPW slots), then the first residual (gateway) row of slots [0, NA);
+//   2. per-lane partial group sums -> LDS;  v := a*x;  gateway terms of slots [0, NA), then the
+//      gathers of slots [NA, RPW) in the registers just freed; members with several residual
+//      entries (rare) gather the rest one by one;
+//   3. cross-wave group sums (LDS), y = v + sum_g c_g S_g, non-temporal stores; a non-finite output
+//      is recomputed from its CSR row per lane (non-finite guard, see csr_refix).
+template <bool OFF32>
+__device__ __forceinline__ const float *qrow(const float *base, int row, int64_t ld, unsigned lo) {
+    // OFF32: every row of a column block lies within 4 GiB of the block base, so the lane's address
+    // is the block base (SGPRs) + a 32-bit offset (one VGPR, global_load ... saddr)
+    if constexpr (OFF32)
+        return reinterpret_cast<const float *>(reinterpret_cast<const char *>(base) +
+                                               ((uint32_t)row * (uint32_t)(ld * 4) + lo * 4u));
+    else
+        return base + (int64_t)row * ld + lo;
+}
+
+template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique_q(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
+    const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
+    const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t n_cg,
+    int64_t n_items, int cpb_shift, int64_t bs_x, int64_t bs_y,
+    const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
+    const float *__restrict__ csr_val) {
+    static_assert(Q * RPW <= 64 && (Q == 1 || Q == 2 || Q == 4), "descriptor lanes");
+    constexpr int LQ = 64 / Q;                 // lanes per clique
+    constexpr int64_t CW = 4 * LQ;             // columns per item
+    constexpr int NA = GA;                     // gateway gathers in flight per batch (the first
+                                               // batch loads behind the member rows)
+    __shared__ float4 red[G][WAVES][kWave];
+    __shared__ float4 tot[G][kWave];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int q = lane / LQ, lc = lane - q * LQ;
+    const int64_t t = blockIdx.x;
+    if (t >= n_items) return;
+    const int64_t local = t >> 3;
+    const int64_t chunk = (local / n_cg) * 8 + (t & 7);
+    const int64_t cg = local % n_cg;
+    if (chunk * CW >= p) return;               // block-uniform, before any barrier
+    const bool act = chunk * CW + 4 * lc < p;  // p % 4 == 0: a lane's 4 columns are all in or out
+    const unsigned lo = act ? (unsigned)(4 * lc) : 0u;
+    const int64_t kb = chunk >> cpb_shift, cin = chunk - (kb << cpb_shift);
+    const float *xc = x + kb * bs_x + cin * CW;
+    float *yc = y + kb * bs_y + cin * CW;
+
+    // descriptors, lane-parallel: lane d < Q*RPW -> (clique cg*Q + d / RPW, slot d % RPW):
+    // d_rg = member row | group << 28 (-1: no member), d_rc = first residual source row (-1: none)
+    int d_rg = -1, d_rc = -1;
+    float d_rv = 0.f, d_cf[1 + G];
+#pragma unroll
+    for (int g = 0; g <= G; ++g) d_cf[g] = 0.f;
+    bool d_multi = false;
+    if (lane < Q * RPW) {
+        const int dq = lane / RPW, dr = lane - (lane / RPW) * RPW;
+        const int64_t c = cg * Q + dq;
+        if (c < n_cliques) {
+            const int32_t m0 = clique_ptr[c], M = clique_ptr[c + 1] - m0;
+            const int k = wave + WAVES * dr;
+            if (k < M) {
+                const int32_t m = m0 + k;
+                d_rg = member_row[m] | ((member_group[m] & kMemberGroupMask) << 28);
+#pragma unroll
+                for (int g = 0; g <= G; ++g) d_cf[g] = coef[(int64_t)m * (1 + G) + g];
+                const int32_t rb = res_ptr[m], rn = res_ptr[m + 1] - rb;
+                d_multi = rn > 1;
+                if (rn > 0) {
+                    d_rc = res_col[rb];
+                    d_rv = res_val[rb];
+                }
+            }
+        }
+    }
+    const bool multi = __ballot(d_multi) != 0;
+    const int sl0 = q * RPW;                   // this lane's descriptor lane of slot 0
+    constexpr int kRowMask = (1 << 28) - 1;
+    // 1. member rows, then the gateway rows of slots [0, NA) (in flight behind them)
+    float v[RPW][4];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int rg = __shfl(d_rg, sl0 + r);
+        ldv<4>(qrow<OFF32>(xc, rg < 0 ? 0 : rg & kRowMask, ld_x, lo), v[r]);
+    }
+    float ga[NA][4];
+#pragma unroll
+    for (int r = 0; r < NA; ++r) {
+        const int rc = __shfl(d_rc, sl0 + r);
+        ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r]);
+    }
+    // every load above is issued before any use below (the scheduler would otherwise fuse the
+    // per-slot loops and serialise the loads slot by slot under the 64-VGPR budget)
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. partial group sums, one group at a time (a slot without a member is masked by rg < 0)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int rg = __shfl(d_rg, sl0 + r);
+            const bool in = rg >= 0 && (rg >> 28) == g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[e] += in ? v[r][e] : 0.f;
+        }
+        red[g][wave][lane] = make_float4(s[0], s[1], s[2], s[3]);
+    }
+    // own terms and the gateway terms of slots [0, NA)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const float a = __shfl(d_cf[0], sl0 + r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[r][e] *= a;
+    }
+#pragma unroll
+    for (int r = 0; r < NA; ++r) {
+        const bool has = __shfl(d_rc, sl0 + r) >= 0;
+        const float w = __shfl(d_rv, sl0 + r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
+    }
+    // gathers of slots [NA, RPW) in batches of NA, in ga's registers
+#pragma unroll
+    for (int b0 = NA; b0 < RPW; b0 += NA) {
+#pragma unroll
+        for (int r = b0; r < RPW && r < b0 + NA; ++r) {
+            const int rc = __shfl(d_rc, sl0 + r);
+            ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r - b0]);
+        }
+#pragma unroll
+        for (int r = b0; r < RPW && r < b0 + NA; ++r) {
+            const bool has = __shfl(d_rc, sl0 + r) >= 0;
+            const float w = __shfl(d_rv, sl0 + r);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r - b0][e], v[r][e]) : v[r][e];
+        }
+    }
+    // members with several residual entries (rare): the rest one by one, per lane
+    if (multi) {
+        const int64_t c = cg * Q + q;
+        const int32_t m0 = c < n_cliques ? clique_ptr[c] : 0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            if (__shfl(d_rg, sl0 + r) < 0) continue;
+            const int32_t m = m0 + wave + WAVES * r;
+            const int rb = res_ptr[m], re = res_ptr[m + 1];
+            for (int j = rb + 1; j < re; ++j) {
+                const float w = res_val[j];
+                float xv[4];
+                ldv<4>(xc + (int64_t)res_col[j] * ld_x + lo, xv);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[r][e] = __builtin_fmaf(w, xv[e], v[r][e]);
+            }
+        }
+    }
+    // 3. group sums across waves
+    __syncthreads();
+    if (wave < G) {
+        float4 a = red[wave][0][lane];
+#pragma unroll 4
+        for (int w = 1; w < WAVES; ++w) {
+            const float4 b = red[wave][w][lane];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        tot[wave][lane] = a;
+    }
+    __syncthreads();
+    float sg[G][4];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float4 a = tot[g][lane];
+        sg[g][0] = a.x; sg[g][1] = a.y; sg[g][2] = a.z; sg[g][3] = a.w;
+    }
+    uint32_t bad = 0;                          // this lane's slots with a non-finite output
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float cg_ = __shfl(d_cf[1 + g], sl0 + r);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[r][e] = __builtin_fmaf(cg_, sg[g][e], v[r][e]);
+        }
+        const int rg = __shfl(d_rg, sl0 + r);
+        if (rg >= 0 && act) {
+            if (finite_v<4>(v[r])) stv_nt<4>(const_cast<float *>(qrow<OFF32>(yc, rg & kRowMask, ld_y, lo)), v[r]);
+            else bad |= 1u << r;
+        }
+    }
+    while (bad) {                              // non-finite guard, per lane (see csr_refix)
+        const int r = __builtin_ctz(bad);
+        bad &= bad - 1;
+        const int64_t row = __shfl(d_rg, sl0 + r) & kRowMask;
+        float o[4];
+        csr_refix<4>(xc, ld_x, lo, true, row, csr_ptr, csr_col, csr_val, o);
+        stv_nt<4>(yc + row * ld_y + lo, o);
     }
 }
 
@@ -1382,10 +1598,14 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     __syncthreads();
     const int64_t col = c0 + 2 * lane;
     const bool ok = lane < rs && col < p;        // p even: a lane's pair is all-in or all-out
+    // LDS column index of this lane: lanes >= rs (120- / 96-column items) compute nothing that is
+    // stored; they re-read column pair rs-1 so that no read leaves the staged row (the last slot
+    // of a group would otherwise read past the dynamic LDS allocation)
+    const int sl = lane < rs ? lane : rs - 1;
     const int tb = grp_tile_ptr[grp], te = grp_tile_ptr[grp + 1];
     typedef __attribute__((address_space(3))) float lds_float;
     const unsigned lds_base = (unsigned)(size_t)(lds_float *)lds_tile;   // LDS byte offset of stage
-    const int lane8 = lane * (int)sizeof(f2);
+    const int lane8 = sl * (int)sizeof(f2);
     for (int sub = tb + wave; sub < te; sub += n_waves) {
         const int li = lane < RT ? lane : RT - 1;
         const int d_row = sub_rows[sub * RT + li];
@@ -1394,7 +1614,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         TileAcc<RT> acc;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
-            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + lane];
+            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + sl];
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
             acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
         }
@@ -1436,7 +1656,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     }
                     if (j < cnt) {                                       // one hard position
                         const int sj = __builtin_amdgcn_readlane(d_src, j);
-                        const f2 xu = stage[(sj & kPosRowMask) * rs + lane];
+                        const f2 xu = stage[(sj & kPosRowMask) * rs + sl];
                         const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(d_mask, j) & FULL;
                         const float wu = __int_as_float(__builtin_amdgcn_readlane(d_wu, j));
                         const float *wp = pos_w + (kb + j) * RT;
@@ -1497,11 +1717,11 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 f2 xa[D], xb[D];
 #pragma unroll
                 for (int u = 0; u < D; ++u)
-                    xa[u] = stage[__builtin_amdgcn_readlane(d_addr, u) + lane];
+                    xa[u] = stage[__builtin_amdgcn_readlane(d_addr, u) + sl];
                 for (int j = 0; j < nd; j += D) {
 #pragma unroll
                     for (int u = 0; u < D; ++u)
-                        xb[u] = stage[__builtin_amdgcn_readlane(d_addr, j + D + u) + lane];
+                        xb[u] = stage[__builtin_amdgcn_readlane(d_addr, j + D + u) + sl];
                     constexpr uint64_t GM = (1ull << D) - 1ull;
                     if (((part_bits >> j) & GM) == 0ull) {        // all D taken by every row
 #pragma unroll
@@ -1517,7 +1737,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     for (int u = 0; u < D; ++u) xa[u] = xb[u];
                 }
                 for (int j = nd; j < cnt; ++j) {                  // the chunk's last cnt % D
-                    const f2 xu = stage[__builtin_amdgcn_readlane(d_addr, j) + lane];
+                    const f2 xu = stage[__builtin_amdgcn_readlane(d_addr, j) + sl];
                     if ((slow_bits >> j) & 1ull) general(j, xu);
                     else step(j, xu);
                 }
@@ -1531,12 +1751,12 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             f2 xa[D], xb[D];
 #pragma unroll
             for (int u = 0; u < D; ++u)
-                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * rs + lane];
+                xa[u] = stage[(__builtin_amdgcn_readlane(d_src, u < cnt ? u : cnt - 1) & kPosRowMask) * rs + sl];
             for (int j = 0; j < cnt; j += D) {
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     const int jn = j + D + u < cnt ? j + D + u : cnt - 1;
-                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * rs + lane];
+                    xb[u] = stage[(__builtin_amdgcn_readlane(d_src, jn) & kPosRowMask) * rs + sl];
                 }
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
@@ -1578,7 +1798,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             if (row < 0) continue;                                  // wave-uniform
             f2 o = acc.get(r);
             if (!avg_only) {
-                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + lane];
+                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + sl];
                 o = xs * 0.f + o;
             }
             if (ok) {
@@ -1717,6 +1937,28 @@ __global__ __launch_bounds__(256) void k_grad_segment_mean(const float *__restri
 }
 
 // ----------------------------------------------------------------------------------------------
+// update_models(all_models, avg) of the 'sample' topology's round (d_sgd.py:246-250 via :29-35):
+// every row y_i := fl(fl(x_i * 0) + avg) (p.mul_(0.); p.add_(new); y == x: in place): avg
+// everywhere, except that a non-finite x_i gives NaN and a zero avg keeps the sign rule of
+// (+-0) + (+-0).
+template <int V>
+__global__ __launch_bounds__(256) void k_update_rows(const float *x, int64_t ld_x, float *y,
+                                                     int64_t ld_y, int64_t n_rows, int64_t p,
+                                                     const float *__restrict__ avg, int64_t n_chunks) {
+    for (int64_t t = blockIdx.x; t < n_rows * n_chunks; t += gridDim.x) {
+        const int64_t r = t / n_chunks;
+        const int64_t c = (t % n_chunks) * (256 * V) + (int64_t)threadIdx.x * V;
+        if (c >= p) continue;
+        float xv[V], av[V];
+        ldv<V>(x + r * ld_x + c, xv);
+        ldv<V>(avg + c, av);
+#pragma unroll
+        for (int e = 0; e < V; ++e) xv[e] = xv[e] * 0.f + av[e];    // two roundings (fp-contract off)
+        stv_nt<V>(y + r * ld_y + c, xv);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // SGD step on listed rows (torch.optim.SGD, momentum 0, no weight decay: param.add_(grad,
 // alpha=-lr), whose ATen CPU kernel computes fma(-lr, g, p) with fp32 alpha — one rounding):
 //   p[row] = fma(neg_lr, g[row], p[row])    for row in rows
@@ -1789,6 +2031,48 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
     return check_launch("k_mix_clique");
 }
 
+// Multi-clique tile (k_mix_clique_q): Q cliques x 64 columns per item, 16 waves x 7 slots (cliques
+// of <= 112 members).  Chosen when a 256-column chunk of all member rows (n_members KB) would not
+// fit an XCD's L2; NIIDMIX_CLIQUE_Q=1 disables it, =4 forces it (A/B).
+constexpr int64_t kQRowsMin = 4096;
+template <int G, int W, int R, int OCC, int GA>
+int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                    const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
+    constexpr int Q = 4;
+    constexpr int64_t CW = 4 * (64 / Q);
+    const int64_t n_cg = (pl->n_cliques + Q - 1) / Q;
+    const int64_t n_chunks = (p + CW - 1) / CW;
+    const int64_t n_items = n_cg * ((n_chunks + 7) / 8) * 8;
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique group, chunk) items for one grid");
+    const int cpb = bg.bc_shift >= 62 ? 62 : bg.bc_shift - 6;
+    // 32-bit row offsets when every block (column-blocked slabs) spans < 4 GiB
+    const bool off32 = bg.bc_shift < 62 && bg.bs_x * 4 <= (int64_t)0xffffffffLL &&
+                       bg.bs_y * 4 <= (int64_t)0xffffffffLL;
+#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
+    if (off32) NIIDMIX_CQ(true); else NIIDMIX_CQ(false);
+#undef NIIDMIX_CQ
+    return check_launch("k_mix_clique_q");
+}
+
+template <int W, int R, int OCC, int GA>
+int launch_clique_q_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
+                      const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
+    switch (pl->n_groups) {
+        case 1: return launch_clique_q<1, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 2: return launch_clique_q<2, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 3: return launch_clique_q<3, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 4: return launch_clique_q<4, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
+        default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
+    }
+}
+
+bool use_clique_q(const niidmix_clique_plan *pl, const BlockGeom &bg) {
+    if (pl->max_clique > 112 || bg.bc_shift < 6) return false;
+    if (bg.bc_shift < 8) return true;          // 64- / 128-column blocks: only this tile reads them
+    if (const char *e = getenv("NIIDMIX_CLIQUE_Q")) return atoi(e) == 4;
+    return pl->n_members >= kQRowsMin;
+}
+
 // Register tile per clique size: WAVES x RPW >= max_clique, OCC = waves/SIMD the register budget
 // targets, RW = residual entries per wave held lane-parallel (gathered in batches, then further
 // chunks of 64), FL = flags (2: non-temporal member loads), V = columns per lane (4: 256-column
@@ -1806,6 +2090,20 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     if (v > vmax) return set_error(NIIDMIX_EINVAL, "%d columns per lane do not fit %d-column blocks", v, 1 << bg.bc_shift);
     const int mc = pl->max_clique;
     if (!vec4) return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
+    if (waves == 0 && use_clique_q(pl, bg)) {
+        // tile: <waves>x<slots>x<occupancy>x<gateway gathers per batch>; NIIDMIX_CLIQUE_QT overrides
+        int qw = 0, qr = 0, qo = 0, qg = 0;
+        if (const char *e = getenv("NIIDMIX_CLIQUE_QT")) sscanf(e, "%dx%dx%dx%d", &qw, &qr, &qo, &qg);
+        if (qw == 0) {
+            if (mc <= 104) { qw = 8; qr = 13; qo = 4; qg = 13; }
+            else { qw = 16; qr = 7; qo = 8; qg = 2; }
+        }
+        if (qw * qr < mc) return set_error(NIIDMIX_EINVAL, "clique tile %dx%d < %d members", qw, qr, mc);
+#define NIIDMIX_QT(W, R, O, GA) if (qw == W && qr == R && qo == O && qg == GA) return launch_clique_q_g<W, R, O, GA>(x, ld_x, y, ld_y, p, pl, s, bg)
+        NIIDMIX_QT(8, 13, 4, 13); NIIDMIX_QT(16, 7, 8, 2); NIIDMIX_QT(16, 7, 8, 3); NIIDMIX_QT(16, 7, 4, 7);
+#undef NIIDMIX_QT
+        return set_error(NIIDMIX_EUNSUPPORTED, "no multi-clique tile %dx%dx%dx%d", qw, qr, qo, qg);
+    }
     if (waves * rpw < mc) {
         rw = 64; ob = 2; v = vmax;  // non-temporal member loads: 1.39 vs 1.47 ms (headline, same box)
         if (mc <= 16) { waves = 8; rpw = 2; occ = 8; }
@@ -2049,7 +2347,8 @@ int niidmix_mix_clique_blocked_f32(const float *x, float *y, int64_t p, int64_t 
         return set_error(NIIDMIX_EINVAL, "null pointer");
     // the register tile's items are 256 columns wide, the big-clique kernel's 32: an item never
     // straddles a block
-    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : 256;
+    // (64 for cliques of <= 112 members: the multi-clique tile's 64-column items)
+    const int64_t min_bc = plan->max_clique > 256 ? kBigRegCols : plan->max_clique <= 112 ? 64 : 256;
     if (block_cols < min_bc || (block_cols & (block_cols - 1)))
         return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= %lld", (long long)block_cols,
                          (long long)min_bc);
@@ -2135,8 +2434,8 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, vec4, s);
 }
 
-int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                         const niidmix_tile_plan *plan, int mode, void *stream) {
+int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                         int64_t p, const niidmix_tile_plan *plan, int mode, void *stream) {
     if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
     const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
     mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
@@ -2150,7 +2449,9 @@ int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
         !plan->pos_mask || !plan->pos_w)
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (n_rows < 1) return set_error(NIIDMIX_EINVAL, "n_rows < 1");
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
     // columns per lane: 4 for 8- and 16-row tiles, 2 for 32-row tiles (register budget);
@@ -2176,8 +2477,8 @@ int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
     return check_launch("k_mix_tile");
 }
 
-int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
-                             const niidmix_tile_lds_plan *plan, int mode, void *stream) {
+int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                             int64_t p, const niidmix_tile_lds_plan *plan, int mode, void *stream) {
     if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
     const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
     mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
@@ -2192,7 +2493,9 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         !plan->pos_slot || !plan->pos_mask || !plan->pos_w)
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (x == y) return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (n_rows < 1) return set_error(NIIDMIX_EINVAL, "n_rows < 1");
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     if (plan->max_src < 1 || plan->max_src > 256)
         return set_error(NIIDMIX_EUNSUPPORTED, "group with %d source rows (1..256 supported)", plan->max_src);
     const int max_waves = tile_lds_max_waves(plan->rt);
@@ -2291,14 +2594,15 @@ int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, fl
     return check_launch("k_row_dist2");
 }
 
-int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y, int64_t p,
-                                  int64_t n_seg, const int32_t *seg_ptr, const int32_t *seg_row,
-                                  void *stream) {
-    if (p < 0 || n_seg < 0) return set_error(NIIDMIX_EINVAL, "negative size");
-    if (n_seg == 0 || p == 0) return NIIDMIX_OK;
+int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_t ld_y,
+                                  int64_t n_rows, int64_t p, int64_t n_seg, const int32_t *seg_ptr,
+                                  const int32_t *seg_row, void *stream) {
+    if (p < 0 || n_seg < 0 || n_rows < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n_seg == 0 || p == 0 || n_rows == 0) return NIIDMIX_OK;
     if (!g || !y || !seg_ptr || !seg_row) return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_g < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
-    if (g == y) return set_error(NIIDMIX_EALIAS, "g and y alias: the mean is out-of-place");
+    if (overlaps(g, (n_rows - 1) * ld_g + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "g and y overlap: the mean is out-of-place");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool vec4 = p % 4 == 0 && ld_g % 4 == 0 && ld_y % 4 == 0 && aligned16(g) && aligned16(y);
     const int64_t cols = vec4 ? 1024 : 256;
@@ -2314,19 +2618,24 @@ int niidmix_grad_segment_mean_f32(const float *g, int64_t ld_g, float *y, int64_
     return check_launch("k_grad_segment_mean");
 }
 
-int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t p, int64_t ld,
-                                          int64_t block_cols, int64_t block_stride_g,
+int niidmix_grad_segment_mean_blocked_f32(const float *g, float *y, int64_t n_rows, int64_t p,
+                                          int64_t ld, int64_t block_cols, int64_t block_stride_g,
                                           int64_t block_stride_y, int64_t n_seg,
                                           const int32_t *seg_ptr, const int32_t *seg_row,
                                           void *stream) {
-    if (p < 0 || n_seg < 0) return set_error(NIIDMIX_EINVAL, "negative size");
-    if (n_seg == 0 || p == 0) return NIIDMIX_OK;
+    if (p < 0 || n_seg < 0 || n_rows < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n_seg == 0 || p == 0 || n_rows == 0) return NIIDMIX_OK;
     if (!g || !y || !seg_ptr || !seg_row) return set_error(NIIDMIX_EINVAL, "null pointer");
     if (block_cols < 1024 || (block_cols & (block_cols - 1)))
         return set_error(NIIDMIX_EINVAL, "block_cols %lld: a power of two >= 1024", (long long)block_cols);
     if (ld < block_cols || block_stride_g < ld || block_stride_y < ld)
         return set_error(NIIDMIX_EINVAL, "row stride < block_cols or block stride < row stride");
-    if (g == y) return set_error(NIIDMIX_EALIAS, "g and y alias: the mean is out-of-place");
+    {   // extents of both blocked slabs, each with its own block stride
+        const int64_t k_blocks = (p + block_cols - 1) / block_cols;
+        if (overlaps(g, (k_blocks - 1) * block_stride_g + (n_rows - 1) * ld + block_cols,
+                     y, (k_blocks - 1) * block_stride_y + (n_rows - 1) * ld + block_cols))
+            return set_error(NIIDMIX_EALIAS, "g and y overlap: the mean is out-of-place");
+    }
     if (p % 4 || ld % 4 || block_stride_g % 4 || block_stride_y % 4 || !aligned16(g) || !aligned16(y))
         return set_error(NIIDMIX_EUNSUPPORTED, "blocked gradient mean needs p, strides % 4 == 0 and 16-B aligned slabs");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2356,6 +2665,29 @@ int niidmix_sgd_step_rows_f32(float *p, int64_t ld_p, const float *g, int64_t ld
     else
         hipLaunchKernelGGL(k_sgd_step_rows<1>, grid, block, 0, s, p, ld_p, g, ld_g, ncols, rows, n_rows, neg_lr, n_chunks);
     return check_launch("k_sgd_step_rows");
+}
+
+int niidmix_update_rows_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                            int64_t p, const float *avg, void *stream) {
+    if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n_rows == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !avg) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    const int64_t ext_x = (n_rows - 1) * ld_x + p, ext_y = (n_rows - 1) * ld_y + p;
+    if (!(x == y && ld_x == ld_y) && overlaps(x, ext_x, y, ext_y))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap without being the same slab");
+    if (overlaps(x, ext_x, avg, p) || overlaps(y, ext_y, avg, p))
+        return set_error(NIIDMIX_EALIAS, "avg overlaps a slab");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool vec4 = p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && aligned16(x) && aligned16(y) &&
+                      aligned16(avg);
+    const int64_t cols = vec4 ? 1024 : 256;
+    const int64_t n_chunks = (p + cols - 1) / cols;
+    const int64_t items = n_rows * n_chunks;
+    const dim3 grid((unsigned)(items < kMaxGrid ? items : kMaxGrid)), block(256);
+    if (vec4) hipLaunchKernelGGL(k_update_rows<4>, grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, avg, n_chunks);
+    else hipLaunchKernelGGL(k_update_rows<1>, grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, avg, n_chunks);
+    return check_launch("k_update_rows");
 }
 
 int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,

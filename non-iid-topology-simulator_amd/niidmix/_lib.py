@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NIIDMIX_LIB", os.path.join(_HERE, "libniidmix.so"))
 
 OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
 MODE_EXACT, MODE_FAST = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
 
@@ -54,17 +54,18 @@ SIGNATURES = {
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                                       ctypes.POINTER(CliquePlanC), _vp]),
-    "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+    "niidmix_mix_tile_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64,
                                             ctypes.POINTER(TilePlanC), ctypes.c_int, _vp]),
-    "niidmix_mix_tile_lds_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
+    "niidmix_mix_tile_lds_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64,
                                                 ctypes.POINTER(TileLdsPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
                                              _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
-    "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp,
-                                                     _vp]),
+    "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp,
+                                                     _vp, _vp]),
     "niidmix_grad_segment_mean_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64,
-                                                             _i64, _i64, _vp, _vp, _vp]),
+                                                             _i64, _i64, _i64, _vp, _vp, _vp]),
+    "niidmix_update_rows_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_sgd_step_rows_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _vp, _i64,
                                                  ctypes.c_float, _vp]),
     "niidmix_hbm_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, _vp]),

@@ -11,9 +11,9 @@ pipelines use it unchanged once params.algorithm.module = 'niidmix.d_sgd':
   average(nodes, topology, params)          -> None, Jacobi mixing of every node's model  (:96-116)
   update_models / average_gradients / update_gradients / gradient       (:19-94)
 
-Only average() changes implementation: the nodes' models become views of one pinned host slab
-(niidmix.slab.NodeSlab), each round streams that slab through HBM in column windows and the HIP
-kernels mix it (niidmix.ops.Mixer).  Mixing mode (params['algorithm']['mixing-mode'], or the
+Only the mixing changes implementation (average(), and the sample topology's uniform average):
+the nodes' models become views of one pinned host slab (niidmix.slab.NodeSlab), each round streams
+that slab through HBM in column windows and the HIP kernels mix it (niidmix.ops.Mixer).  Mixing mode (params['algorithm']['mixing-mode'], or the
 NIIDMIX_MODE environment variable):
   'exact' (default)  bit-identical to the reference loop (tests/test_gpu_dropin.py)
   'fast'             clique-factored / MFMA kernels, within 1e-5 condition-aware relative
@@ -105,6 +105,48 @@ def _grad_key(params):
 
 
 _grad_engines = {}
+
+
+class _SampleEngine:
+    """NodeSlab of EVERY node + SampleAverage streamed by SlabMixer (one column stripe per GPU)."""
+
+    def __init__(self, nodes, devices):
+        from .slab import MultiDeviceRound, NodeSlab, SampleAverage, SlabMixer
+        self.slab = NodeSlab([n["model"] for n in nodes])
+        self.ops = []
+
+        def make(dev, n, cols):
+            op = SampleAverage(dev)
+            self.ops.append(op)
+            return SlabMixer(op, n, cols, dev, window=_window())
+        self.runner = MultiDeviceRound(make, self.slab.n, self.slab.p, devices)
+
+    def run(self, ranks, weights):
+        for op in self.ops:
+            op.set_active(ranks, weights)
+        self.runner.run(self.slab.host, mode="exact")
+
+    def owns(self, nodes):
+        return self.slab.owns([n["model"] for n in nodes])
+
+
+_sample_engines = {}
+
+
+def sample_average(all_nodes, active):
+    """The 'sample' topology's round after the active nodes' optimizer steps (d_sgd.py:240-250):
+    avg = setup.model.average([active models], [1/len(active)]*len(active)), then
+    update_models([every model], avg) — one device round over the pinned slab of every node
+    (niidmix.slab.SampleAverage), bit for bit the reference's CPU arithmetic."""
+    key = id(all_nodes)
+    eng = _sample_engines.get(key)
+    if eng is None or not eng.owns(all_nodes):
+        eng = _SampleEngine(all_nodes, _devices(all_nodes))
+        _sample_engines.clear()
+        _sample_engines[key] = eng
+    pos = {id(n): i for i, n in enumerate(all_nodes)}
+    logging.info("  computing average model of sample consisting of %d nodes (GPU)", len(active))
+    eng.run([pos[id(n)] for n in active], [1 / len(active) for _ in active])
 
 
 def gradient(nodes, topology, params):
@@ -356,11 +398,14 @@ def randomized_topology(nodes, params, rundir):
     incremented topology-seed), built SPARSE: the edge lists by the restated generator
     (niidmix.generate.random_graph, same RNG order, hence the same graph) and the MH weights as a
     CSR (topology.mh_csr, bit-identical to compute_weights) -- O(N k) weights instead of the dense
-    N x N matrix.  The rundir gets topology.csr.npz every round, and the reference's dense
-    topology.json as well up to NIIDMIX_DENSE_JSON_MAX nodes (default 1024; niidmix.topology.load
-    reads whichever is newer)."""
+    N x N matrix.  Every round the rundir gets topology.json (d_sgd.py:229-230), always readable
+    by the reference's loader: up to NIIDMIX_DENSE_JSON_MAX nodes (default 1024) with the dense
+    weights the reference writes, above it in the sparse form (niidmix.topology.sparse_json:
+    'weights': [] + the CSR in topology.csr.npz), so the file never lags the graph the round used.
+    The returned topology carries the weights as the reference's does (a dense tensor, or the
+    empty tensor the loader makes of the sparse form) plus the CSR under 'csr'."""
     from .generate import random_graph_csr
-    from .topology import save_csr
+    from .topology import sparse_json, save_csr
     t = params["topology"]
     weights = t.get("weights", "metropolis-hasting")
     if weights != "metropolis-hasting":
@@ -369,13 +414,15 @@ def randomized_topology(nodes, params, rundir):
     n = len(nodes)
     assert [nd["rank"] for nd in nodes] == list(range(n)), "nodes must be listed in rank order"
     csr, edges = random_graph_csr(n, t["nb-neighbours"], t["topology-seed"])
+    dense = n <= DENSE_JSON_MAX
+    w = csr.dense() if dense else None
     if rundir is not None:
         save_csr(os.path.join(rundir, "topology.csr.npz"), csr)
-        if n <= DENSE_JSON_MAX:
-            with open(os.path.join(rundir, "topology.json"), "w+") as f:
-                json.dump({"edges": {r: edges[r] for r in edges},
-                           "weights": csr.dense().tolist()}, f)
-    return {"edges": edges, "csr": csr, "weights": None}
+        with open(os.path.join(rundir, "topology.json"), "w+") as f:
+            json.dump({"edges": {r: edges[r] for r in edges}, "weights": w.tolist()} if dense
+                      else sparse_json(edges), f)
+    return {"edges": edges, "csr": csr,
+            "weights": torch.from_numpy(w) if dense else torch.tensor([])}
 
 
 def next_step(state, params, rundir):
@@ -411,9 +458,7 @@ def next_step(state, params, rundir):
     else:
         for n in active:
             n["optimizer"].step()
-        center = nm.average([n["model"] for n in active],
-                            [1 / len(active) for _ in active])
-        update_models([n["model"] for n in state["nodes"]], center)
+        sample_average(state["nodes"], active)            # ★ GPU: average + update_models
     state["step"] += 1
     return state, losses, epoch_done, active
 

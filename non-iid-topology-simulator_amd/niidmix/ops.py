@@ -77,6 +77,21 @@ def _no_overlap(a, b):
     _req(a1 <= b0 or b1 <= a0, "x and out overlap: mixing is out-of-place (Jacobi, d_sgd.py:99-116)")
 
 
+def _blocked_no_overlap(a, b, msg):
+    """Two column-blocked [K, rows, B] slabs must not share a byte: each one's extent from its OWN
+    block and row strides (the two may differ in block stride)."""
+    if a.numel() == 0 or b.numel() == 0:
+        return
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return
+
+    def ext(t):
+        k, rows, bc = t.shape
+        return ((k - 1) * t.stride(0) + (rows - 1) * t.stride(1) + bc) * 4
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    _req(a0 + ext(a) <= b0 or b0 + ext(b) <= a0, msg)
+
+
 def _ld(t):
     return t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
 
@@ -157,10 +172,7 @@ def mix_clique_blocked(x: torch.Tensor, clique_ptr: torch.Tensor, member_row: to
     k, rows, b = x.shape
     _req(0 <= p <= k * b and (k == 0 or p > (k - 1) * b), f"p={p} does not fit {k} blocks of {b}")
     _req(member_row.device == x.device, "plan and slabs must be on the same device")
-    if x.numel() and x.untyped_storage().data_ptr() == out.untyped_storage().data_ptr():
-        ext = ((k - 1) * x.stride(0) + (rows - 1) * x.stride(1) + b) * 4
-        x0, o0 = x.data_ptr(), out.data_ptr()
-        _req(x0 + ext <= o0 or o0 + ext <= x0, "x and out overlap: mixing is out-of-place")
+    _blocked_no_overlap(x, out, "x and out overlap: mixing is out-of-place")
     plan = _clique_plan_c(clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val,
                           res_member, row_ptr, col, val, max_clique, max_clique_res)
     rc = _lib.lib.niidmix_mix_clique_blocked_f32(x.data_ptr(), out.data_ptr(), int(p), x.stride(1),
@@ -190,8 +202,8 @@ def mix_tile(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
     plan = _lib.TilePlanC(t, int(rt), 0, sub_ptr.data_ptr(), sub_rows.data_ptr(),
                           sub_wself.data_ptr(), pos_src.data_ptr() or some,
                           pos_mask.data_ptr() or some, pos_w.data_ptr() or some)
-    rc = _lib.lib.niidmix_mix_tile_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), x.shape[1],
-                                       ctypes.byref(plan), int(mode), _stream(x))
+    rc = _lib.lib.niidmix_mix_tile_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), out.shape[0],
+                                       x.shape[1], ctypes.byref(plan), int(mode), _stream(x))
     _lib.check(rc, "niidmix::mix_tile")
 
 
@@ -224,7 +236,8 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                              pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
                              grp_src_ptr.data_ptr(), grp_src_rows.data_ptr())
     rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
-                                           x.shape[1], ctypes.byref(plan), int(mode), _stream(x))
+                                           out.shape[0], x.shape[1], ctypes.byref(plan), int(mode),
+                                           _stream(x))
     _lib.check(rc, "niidmix::mix_tile_lds")
 
 
@@ -271,8 +284,9 @@ def grad_segment_mean(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: torch.Ten
     _vec("seg_ptr", seg_ptr, torch.int32, dev)
     _vec("seg_row", seg_row, torch.int32, dev)
     _no_overlap(g, out)
+    _req(out.shape[0] == g.shape[0], "g and out: same rows")
     rc = _lib.lib.niidmix_grad_segment_mean_f32(g.data_ptr(), _ld(g), out.data_ptr(), _ld(out),
-                                                g.shape[1], seg_ptr.numel() - 1,
+                                                g.shape[0], g.shape[1], seg_ptr.numel() - 1,
                                                 seg_ptr.data_ptr(), seg_row.data_ptr(), _stream(g))
     _lib.check(rc, "niidmix::grad_segment_mean")
 
@@ -290,11 +304,27 @@ def grad_segment_mean_blocked(g: torch.Tensor, seg_ptr: torch.Tensor, seg_row: t
     _req(0 <= p <= k * b and (k == 0 or p > (k - 1) * b), f"p={p} does not fit {k} blocks of {b}")
     _vec("seg_ptr", seg_ptr, torch.int32, g.device)
     _vec("seg_row", seg_row, torch.int32, g.device)
-    _req(g.data_ptr() != out.data_ptr(), "g and out overlap: the mean is out-of-place")
+    _blocked_no_overlap(g, out, "g and out overlap: the mean is out-of-place")
     rc = _lib.lib.niidmix_grad_segment_mean_blocked_f32(
-        g.data_ptr(), out.data_ptr(), int(p), g.stride(1), b, g.stride(0), out.stride(0),
+        g.data_ptr(), out.data_ptr(), rows, int(p), g.stride(1), b, g.stride(0), out.stride(0),
         seg_ptr.numel() - 1, seg_ptr.data_ptr(), seg_row.data_ptr(), _stream(g))
     _lib.check(rc, "niidmix::grad_segment_mean_blocked")
+
+
+@torch.library.custom_op("niidmix::update_rows", mutates_args=("out",))
+def update_rows(x: torch.Tensor, avg: torch.Tensor, out: torch.Tensor) -> None:
+    """out[i] = fl(fl(x[i] * 0) + avg) for every row (out may be x itself): update_models(all_models,
+    avg) of the 'sample' topology's round (d_sgd.py:246-250, :29-35)."""
+    _slab("x", x)
+    _slab("out", out, rows=x.shape[0], cols=x.shape[1])
+    _req(avg.device == x.device and out.device == x.device and avg.dtype == torch.float32 and
+         avg.dim() == 1 and avg.numel() == x.shape[1] and avg.is_contiguous(),
+         "avg: expected contiguous fp32 [p] on the slab's device")
+    if not (out.data_ptr() == x.data_ptr() and _ld(out) == _ld(x)):
+        _no_overlap(x, out)
+    rc = _lib.lib.niidmix_update_rows_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
+                                          x.shape[0], x.shape[1], avg.data_ptr(), _stream(x))
+    _lib.check(rc, "niidmix::update_rows")
 
 
 @torch.library.custom_op("niidmix::sgd_step_rows", mutates_args=("p",))

@@ -256,6 +256,42 @@ class FusedRoundRunner:
         self.s_d2h.synchronize()
 
 
+class SampleAverage:
+    """The 'sample' topology's round as a per-window device op (d_sgd.py:235-250): the average of
+    the active nodes' rows, setup.model.average(models, [1/k]*k) (model/__init__.py:15-25: exact
+    CSR kernel, one output row, NIIDMIX_FLAG_AVERAGE_ONLY, weights fp32(1/k) in the sample's
+    order), then update_models(all_models, avg) of EVERY row (d_sgd.py:29-35: k_update_rows).
+    Callable like a Mixer, so SlabMixer / MultiDeviceRound stream the pinned slab through it: one
+    H2D and one D2H of the slab per round, no host-side stacking or per-tensor CPU updates."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.row_ptr = self.col = self.val = None
+        self._avg = None
+
+    def set_active(self, rows, weights):
+        import numpy as np
+        k = len(rows)
+        if k == 0:
+            raise ValueError("sample round with no active node")
+        w = np.asarray([float(v) for v in weights], np.float64).astype(np.float32)
+        self.row_ptr = torch.tensor([0, k], dtype=torch.int64, device=self.device)
+        self.col = torch.tensor(list(rows), dtype=torch.int32, device=self.device)
+        self.val = torch.from_numpy(w).to(self.device)
+
+    def __call__(self, x, out=None, mode="exact", kernel=None):
+        from . import ops
+        if out is None:
+            out = torch.empty_like(x)
+        cols = x.shape[1]
+        if self._avg is None or self._avg.shape[1] < cols:
+            self._avg = torch.empty((1, cols), dtype=torch.float32, device=self.device)
+        avg = self._avg[:, :cols]
+        ops.mix_csr(x, self.row_ptr, self.col, self.val, avg, ops.EXACT | ops.AVERAGE_ONLY)
+        ops.update_rows(x, avg[0], out)
+        return out
+
+
 # ------------------------------------------------------------------------------------------------
 # several GPUs in ONE process (the simulator is one process, run.py:136)
 MIN_STRIPE_COLS = 1 << 16

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Sparse topology writer: the reference's topology generator CLIs, emitting
-topology.csr.npz instead of the dense N x N topology.json.
+the weights as a CSR (topology.csr.npz) instead of a dense N x N matrix inside topology.json.
 
     python -m niidmix.sparse_topology d-cliques    [--rundir R] [--interclique fully-connected]
                                                    [--max-clique-size 30] [--remove-clique-edges 0]
@@ -11,18 +11,20 @@ Same arguments, defaults and params.json 'topology' section as the reference CLI
 same graph (niidmix.generate restates the generators with the same RNG order; tests pin it), same
 Metropolis-Hastings weights bit for bit (niidmix.topology.mh_csr), but O(N * degree) memory and
 time for the weights: a 10 000-node d-cliques topology is ~12 MB of CSR instead of a ~1 GB JSON of
-a dense matrix.  niidmix.topology.load(rundir) (the drop-in loader the plugin and tests use) reads
-topology.csr.npz; the rundir's nodes.json gives N, params.json 'meta' the seed, as in the
-reference.  Like the reference CLIs it prints the rundir for the next pipeline stage when --rundir
-is not given.
+a dense matrix.  It also writes a topology.json that the reference's own loader reads unchanged
+(setup.topology.load, called by the unchanged run.py:92-93): 'edges' and 'cliques' as the
+reference writes them, 'weights': [] (an empty tensor once loaded) and 'weights-kind' /
+'weights-csr' naming the Metropolis-Hastings CSR next to it; the plugin (niidmix.d_sgd) mixes
+such a topology through niidmix.topology.to_csr, bit for bit the dense round.  The rundir's
+nodes.json gives N, params.json 'meta' the seed, as in the reference.  Like the reference CLIs it
+prints the rundir for the next pipeline stage when --rundir is not given.
 """
 import argparse
 import logging
-import os
 
 from . import meta as m
 from .generate import dcliques_csr, random_graph_csr
-from .topology import save_csr
+from .topology import write_sparse
 
 
 def _nodes(rundir):
@@ -46,7 +48,7 @@ def d_cliques(args, rundir):
         raise SystemExit("fractal interclique: only the 10-class grouping is restated")
     csr, cliques = dcliques_csr(n, args.max_clique_size, args.interclique, seed,
                                 args.remove_clique_edges)
-    save_csr(os.path.join(rundir, "topology.csr.npz"), csr, cliques)
+    write_sparse(rundir, csr, cliques=cliques)
     logging.info("d-cliques: %d nodes, %d cliques, nnz %d", n, len(cliques), csr.nnz)
 
 
@@ -58,12 +60,12 @@ def random_graph(args, rundir):
                "topology-seed": params["meta"]["seed"]}
     m.extend(rundir, "topology", section)
     csr, _ = random_graph_csr(n, args.nb_neighbours, section["topology-seed"])
-    save_csr(os.path.join(rundir, "topology.csr.npz"), csr)
+    write_sparse(rundir, csr)
     logging.info("random-graph: %d nodes, nnz %d", n, csr.nnz)
 
 
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="Generate a topology as a sparse CSR (topology.csr.npz).")
+    ap = argparse.ArgumentParser(description="Generate a topology with sparse weights (topology.csr.npz + a sparse topology.json).")
     sub = ap.add_subparsers(dest="kind", required=True)
     dc = sub.add_parser("d-cliques", help="random_cliques.py equivalent")
     dc.add_argument("--rundir", type=str, default=None)

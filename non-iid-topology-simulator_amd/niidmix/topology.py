@@ -37,16 +37,61 @@ def load_file(path):
     return topology
 
 
+SPARSE_KIND = "metropolis-hasting"     # the only weights a sparse topology.json stands for
+CSR_FILE = "topology.csr.npz"
+
+
+def sparse_json(edges, cliques=None, csr_file=CSR_FILE, extra=None):
+    """topology.json content for a topology whose weights are NOT stored densely: the reference
+    loader (setup.topology.load, topology/__init__.py:4-12) reads it unchanged -- 'edges' as usual,
+    'weights': [] becomes an empty tensor -- and every reference consumer other than d_sgd.average
+    (which the plugin replaces) reads only edges / cliques (analyze/topology.py).  The mixing
+    weights are the Metropolis-Hastings weights of the edges ('weights-kind'; to_csr rebuilds them
+    bit for bit with mh_csr) and the same CSR sits next to the file ('weights-csr')."""
+    topo = {"edges": {str(r): [int(j) for j in edges[r]] for r in edges}, "weights": [],
+            "weights-kind": SPARSE_KIND, "weights-csr": csr_file}
+    if cliques is not None:
+        topo["cliques"] = [[int(r) for r in c] for c in cliques]
+    if extra:
+        topo.update(extra)
+    return topo
+
+
+def write_sparse(rundir, csr, edges=None, cliques=None):
+    """Write a sparse topology into `rundir`: topology.csr.npz first, then a topology.json the
+    reference loader reads (sparse_json), so the unchanged run.py:92-93 (setup.topology.load)
+    hands the plugin a topology it can mix."""
+    save_csr(os.path.join(rundir, CSR_FILE), csr, cliques)
+    with open(os.path.join(rundir, "topology.json"), "w+") as f:
+        json.dump(sparse_json(edges if edges is not None else csr.edges(), cliques), f)
+
+
+def _empty_weights(w):
+    if w is None:
+        return True
+    if isinstance(w, torch.Tensor):
+        return w.numel() == 0
+    return len(w) == 0
+
+
 def load(rundir):
-    """Drop-in for setup.topology.load(rundir).  If the rundir holds a sparse companion
-    (topology.csr.npz, written by save_csr / niidmix.sparse_topology) that is newer than
-    topology.json (or there is no topology.json), the sparse form is returned under
-    topology['csr'] (weights None) with 'edges' rebuilt from it."""
+    """Drop-in for setup.topology.load(rundir).  A sparse topology.json (sparse_json: empty
+    'weights') gets its companion CSR attached as topology['csr'] when the rundir holds it; a
+    rundir with only topology.csr.npz (or a companion newer than a dense topology.json, as older
+    --randomize rundirs left them) is read from the CSR with 'edges' rebuilt from it."""
     path = os.path.join(rundir, "topology.json")
-    sparse = os.path.join(rundir, "topology.csr.npz")
-    if os.path.exists(path) and not (os.path.exists(sparse) and
-                                     os.path.getmtime(sparse) > os.path.getmtime(path)):
-        return load_file(path)
+    sparse = os.path.join(rundir, CSR_FILE)
+    if os.path.exists(path):
+        topo = load_file(path)
+        if _empty_weights(topo["weights"]) and topo["edges"]:
+            comp = os.path.join(rundir, topo.get("weights-csr", CSR_FILE))
+            if os.path.exists(comp):
+                csr, _ = load_csr(comp)
+                if csr.n == len(topo["edges"]):
+                    topo["csr"] = csr
+            return topo
+        if not (os.path.exists(sparse) and os.path.getmtime(sparse) > os.path.getmtime(path)):
+            return topo
     if os.path.exists(sparse):
         csr, cliques = load_csr(sparse)
         topo = {"edges": csr.edges(), "csr": csr, "weights": None}
@@ -127,10 +172,27 @@ class MixCSR:
 
 
 def to_csr(topology):
-    """CSR of W^T in d_sgd.average's operand order (d_sgd.py:105-106)."""
-    if "csr" in topology and topology.get("weights") is None:
-        return topology["csr"]
-    W = topology["weights"]
+    """CSR of W^T in d_sgd.average's operand order (d_sgd.py:105-106).
+
+    Sparse topologies: with no dense weights (None, or the empty tensor the reference loader makes
+    of a sparse topology.json's 'weights': []) the CSR comes from topology['csr'] when present,
+    else it is rebuilt from the edges with mh_csr (bitwise compute_weights' Metropolis-Hastings
+    weights; 'weights-kind' must say so)."""
+    W = topology.get("weights")
+    if _empty_weights(W):
+        if "csr" in topology:
+            return topology["csr"]
+        edges = topology["edges"]
+        if not edges:
+            return MixCSR(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.float32))
+        kind = topology.get("weights-kind")
+        if kind != SPARSE_KIND:
+            raise ValueError(f"topology has no weights and weights-kind {kind!r}: only "
+                             f"{SPARSE_KIND!r} weights are rebuilt from the edges")
+        n = len(edges)
+        if sorted(edges) != list(range(n)):
+            raise ValueError("sparse topology: edges must list every rank 0..N-1")
+        return mh_csr(n, edges)
     Wn = W.numpy() if isinstance(W, torch.Tensor) else np.asarray(W, np.float32)
     Wn = np.asarray(Wn, np.float32)
     edges = topology["edges"]
@@ -175,38 +237,61 @@ def _check_stochastic(w):
 
 def mh_csr(n, edges):
     """Sparse Metropolis-Hastings straight to the mixing CSR, without materialising the N x N JSON.
-    Values are bit-identical to compute_weights: each off-diagonal is the same fp32 rounding of
-    1./(max(d_i,d_j)+1); the diagonal repeats the reference's fp32 reduction of the dense row
-    W[i,:] (a zero row buffer with the row's entries scattered in, then torch .sum()), so the
-    summation order - and hence every bit - matches weights.py:25.  MH weights are symmetric
-    (W[j,i] = W[i,j]), so row i of W^T holds the same values as row i of W."""
-    deg = np.asarray([len(edges[i]) for i in range(n)], np.int64)
-    sets = [set(edges[i]) for i in range(n)]
-    row = torch.zeros(n)
-    counts = np.empty(n, np.int64)
-    cols, vals = [], []
-    for i in range(n):
-        nb = np.asarray([j for j in edges[i] if j != i], np.int64)
-        off = (1.0 / (np.maximum(deg[i], deg[nb]) + 1)).astype(np.float32) if len(nb) else \
-            np.zeros(0, np.float32)
-        if len(nb):
-            idx = torch.from_numpy(nb)
-            row[idx] = torch.from_numpy(off)
-        diag = (1. - row.sum()).item()
-        if len(nb):
-            row[idx] = 0.0
-        # W[src, i] for src in edges[i] (edges order): row src of W holds i iff i in edges[src]
-        e = list(edges[i])
-        ev = np.asarray([np.float32(diag) if j == i else
-                         (1.0 / (max(deg[i], deg[j]) + 1) if i in sets[j] else 0.0)
-                         for j in e], np.float64).astype(np.float32)
-        cols.append(np.asarray([i] + e, np.int64))
-        vals.append(np.concatenate([np.asarray([diag], np.float32), ev]))
-        counts[i] = 1 + len(e)
+    Values are bit-identical to compute_weights (weights.py:15-25):
+      * each off-diagonal W[i, j] (j in edges[i], j != i) is the fp32 rounding of the double
+        1./(max(d_i, d_j) + 1), d = len(edges[.]);
+      * the diagonal repeats the reference's fp32 reduction of the dense row W[i, :]: rows are
+        scattered into a zero [B, N] buffer and reduced with torch's row sum, which is the same
+        per-row reduction as the reference's 1-D W[i, :].sum() (the summation order, and hence
+        every bit; tests/test_topology.py pins it on every golden topology);
+      * entry (row i, src) of the CSR is W[src, i]: 1./(max(d_i, d_src) + 1) if i in edges[src],
+        else 0 (the reference sets W[src, i] only along src's own edge list).
+    Cost: O(N * degree) vectorised host work for the CSR, plus the diagonal's reduction over the
+    dense rows, O(N^2) fp32 adds in [B, N] batches (the price of bitwise equality with the dense
+    reduction: 10 000 nodes ~0.1 s)."""
+    lens = np.asarray([len(edges[i]) for i in range(n)], np.int64)
+    deg = lens
+    src_of = np.repeat(np.arange(n, dtype=np.int64), lens)                 # row owning the entry
+    dst = np.fromiter((j for i in range(n) for j in edges[i]), np.int64, int(lens.sum()))
+    if dst.size and (dst.min() < 0 or dst.max() >= n):
+        raise ValueError("edge endpoint out of range")
+    off_mask = dst != src_of
+    # W[i, j] for the reference's edge list of i (self entries skipped, weights.py:18-20)
+    wi, wj = src_of[off_mask], dst[off_mask]
+    wv = (1.0 / (np.maximum(deg[wi], deg[wj]) + 1)).astype(np.float32)
+    diag = np.empty(n, np.float32)
+    bsz = int(max(1, min(n, (1 << 25) // max(n, 1))))
+    if n:
+        starts = np.searchsorted(wi, np.arange(0, n, bsz))
+        starts = np.append(starts, wi.size)
+        buf = torch.zeros((bsz, n))
+        for k, r0 in enumerate(range(0, n, bsz)):
+            r1 = min(n, r0 + bsz)
+            a, b = starts[k], starts[k + 1]
+            ri = torch.from_numpy(wi[a:b] - r0)
+            ci = torch.from_numpy(wj[a:b])
+            buf[ri, ci] = torch.from_numpy(wv[a:b])
+            diag[r0:r1] = (1. - buf[:r1 - r0].sum(1)).numpy()
+            buf[ri, ci] = 0.0
+    # CSR of W^T in d_sgd.average's operand order: row i = [i] + edges[i]; value W[src, i]
+    keys = np.unique(wi * n + wj) if wi.size else np.zeros(0, np.int64)   # W[a, b] != 0 pairs
+    rows, srcs = src_of, dst                                              # entry (row i, src)
+    has = np.isin(srcs * n + rows, keys) if keys.size else np.zeros(rows.size, bool)
+    ev = np.where(has, 1.0 / (np.maximum(deg[rows], deg[srcs]) + 1), 0.0).astype(np.float32)
+    self_ent = srcs == rows
+    ev[self_ent] = diag[rows[self_ent]]
+    counts = 1 + lens
     row_ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-    col = np.concatenate(cols).astype(np.int32) if n else np.zeros(0, np.int32)
-    val = np.concatenate(vals).astype(np.float32) if n else np.zeros(0, np.float32)
-    return MixCSR(row_ptr, col, val).validate()
+    col = np.empty(int(row_ptr[-1]), np.int64)
+    val = np.empty(int(row_ptr[-1]), np.float32)
+    heads = row_ptr[:-1]
+    col[heads] = np.arange(n)
+    val[heads] = diag
+    body = np.ones(int(row_ptr[-1]), bool)
+    body[heads] = False
+    col[body] = srcs
+    val[body] = ev
+    return MixCSR(row_ptr, col.astype(np.int32), val).validate()
 
 
 def save_csr(path, csr, cliques=None):

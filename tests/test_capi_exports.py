@@ -74,25 +74,38 @@ def test_argument_errors_without_gpu():
     rc = L.niidmix_mix_dense_f32(16, 4, 1024, 4, 4, 4, 8, None, 8, 8, None)
     assert rc == _lib.EINVAL         # dense: the CSR (non-finite guard) is required
     tp = _lib.TilePlanC(1, 12, 0, 8, 8, 8, 8, 8, 8)
-    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 0, None)
+    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 1, 4, ctypes.byref(tp), 0, None)
     assert rc == _lib.EUNSUPPORTED   # tile height 12
     tp = _lib.TilePlanC(1, 16, 0, None, 8, 8, 8, 8, 8)
-    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 0, None)
+    rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 1, 4, ctypes.byref(tp), 0, None)
     assert rc == _lib.EINVAL         # null sub_ptr
     tp = _lib.TilePlanC(1, 16, 0, 8, 8, 8, 8, 8, 8)
-    assert L.niidmix_mix_tile_f32(16, 4, 1024, 4, 4, ctypes.byref(tp), 9, None) == _lib.EINVAL
-    assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
-    assert L.niidmix_grad_segment_mean_f32(None, 4, 16, 4, 4, 1, 8, 8, None) == _lib.EINVAL
-    assert L.niidmix_grad_segment_mean_f32(16, 4, 16, 4, 4, 1, 8, 8, None) == _lib.EALIAS
-    assert L.niidmix_grad_segment_mean_f32(16, 2, 1024, 4, 4, 1, 8, 8, None) == _lib.EINVAL
-    assert L.niidmix_grad_segment_mean_f32(16, 4, 1024, 4, 4, 0, 8, 8, None) == _lib.OK
+    assert L.niidmix_mix_tile_f32(16, 4, 1024, 4, 1, 4, ctypes.byref(tp), 9, None) == _lib.EINVAL
+    assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 1, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
+    # ABI 3: partial overlaps are caught over the full [n_rows, ld] extents (4 rows of ld 8)
+    assert L.niidmix_mix_tile_f32(base, 8, base + 4 * 20, 8, 4, 8, ctypes.byref(tp), 0, None) == _lib.EALIAS
+    lp = _lib.TileLdsPlanC(1, 16, 1, 8, 1, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)
+    assert L.niidmix_mix_tile_lds_f32(base, 8, base + 4 * 20, 8, 4, 8, ctypes.byref(lp), 0, None) == _lib.EALIAS
+    G = L.niidmix_grad_segment_mean_f32
+    assert G(None, 4, 16, 4, 1, 4, 1, 8, 8, None) == _lib.EINVAL
+    assert G(16, 4, 16, 4, 1, 4, 1, 8, 8, None) == _lib.EALIAS
+    assert G(16, 2, 1024, 4, 1, 4, 1, 8, 8, None) == _lib.EINVAL
+    assert G(16, 4, 1024, 4, 1, 4, 0, 8, 8, None) == _lib.OK
+    assert G(base, 8, base + 4 * 20, 8, 4, 8, 1, 8, 8, None) == _lib.EALIAS   # partial overlap
     B = L.niidmix_grad_segment_mean_blocked_f32
-    assert B(None, 1024, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL    # null
-    assert B(16, 1024, 4, 1024, 1000, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL      # block_cols
-    assert B(16, 1024, 4, 1024, 1024, 512, 4096, 1, 8, 8, None) == _lib.EINVAL       # stride
-    assert B(16, 16, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EALIAS
-    assert B(16, 1024, 6, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EUNSUPPORTED  # p % 4
-    assert B(16, 1024, 4, 1024, 1024, 4096, 4096, 0, 8, 8, None) == _lib.OK         # empty
+    assert B(None, 1024, 1, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL    # null
+    assert B(16, 1024, 1, 4, 1024, 1000, 4096, 4096, 1, 8, 8, None) == _lib.EINVAL      # block_cols
+    assert B(16, 1024, 1, 4, 1024, 1024, 512, 4096, 1, 8, 8, None) == _lib.EINVAL       # stride
+    assert B(16, 16, 1, 4, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EALIAS
+    assert B(16, 1 << 30, 1, 6, 1024, 1024, 4096, 4096, 1, 8, 8, None) == _lib.EUNSUPPORTED  # p % 4
+    assert B(16, 1024, 1, 4, 1024, 1024, 4096, 4096, 0, 8, 8, None) == _lib.OK         # empty
+    # y with a LARGER block stride than g: g's 2 blocks at base + 8 KB, y's block 1 at base + 12 KB
+    assert B(base + 8192, base, 1, 2048, 1024, 1024, 1024, 3072, 1, 8, 8, None) == _lib.EALIAS
+    U = L.niidmix_update_rows_f32
+    assert U(None, 4, 1024, 4, 1, 4, 8, None) == _lib.EINVAL
+    assert U(base, 8, 1 << 30, 8, 4, 8, base + 4 * 20, None) == _lib.EALIAS   # avg inside x
+    assert U(base, 8, base + 4 * 20, 8, 4, 8, 1 << 30, None) == _lib.EALIAS   # partial x / y overlap
+    assert U(base, 8, base, 8, 0, 8, 8, None) == _lib.OK                       # no rows
     rc = L.niidmix_copy2d_async(None, 4, None, 4, 4, 1, 0, None)
     assert rc == _lib.EINVAL
     assert L.niidmix_stream_copy_f32(16, 1024, 6, None) == _lib.EUNSUPPORTED   # n % 4

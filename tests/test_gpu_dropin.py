@@ -374,3 +374,126 @@ def test_randomize_keeps_slab(gpu, oracle_mod):
         assert oracle_mod.bitwise_equal(after, ref)
         params["topology"]["topology-seed"] += 1
         topo = d_sgd.randomized_topology(nodes, params, None)
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+def test_sparse_topology_plugin_round(mode, gpu, oracle_mod, tmp_path, monkeypatch):
+    """Sparse ingestion under the unchanged run.py: a rundir written by niidmix.sparse_topology,
+    read by the reference loader's restatement (load_file; run.py:92-93 -> setup.topology.load,
+    so 'weights' is an EMPTY tensor), mixed by the plugin's average(): exact mode bit for bit the
+    reference's dense-W round (golden dcliques300_fc_p37), fast mode within the tolerance."""
+    import os
+    from niidmix import d_sgd, sparse_topology, topology
+    (tmp_path / "nodes.json").write_text(json.dumps([{"rank": r} for r in range(300)]))
+    (tmp_path / "params.json").write_text(json.dumps({"meta": {"seed": 1337, "log": "WARNING"},
+                                                      "dataset": {"nb-classes": 10}}))
+    sparse_topology.main(["d-cliques", "--rundir", str(tmp_path), "--max-clique-size", "30"])
+    topo = topology.load_file(os.path.join(str(tmp_path), "topology.json"))
+    assert topo["weights"].numel() == 0
+    g = load_golden("dcliques300_fc_p37")
+    nodes, _ = _nodes_and_topology(g)
+    monkeypatch.setenv("NIIDMIX_MODE", mode)
+    d_sgd.average(nodes, topo, {})
+    y = _params_of(nodes)
+    if mode == "exact":
+        assert oracle_mod.bitwise_equal(y, g["y"])
+    else:
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=1e-5)
+        assert ok, worst
+
+
+def _ref_sample_round(all_nodes, active):
+    """The reference's 'sample' branch after the optimizer steps (d_sgd.py:240-250), restated with
+    torch CPU ops: setup.model.average (deepcopy, mul_(0), add_(w*p); model/__init__.py:15-25)
+    then update_models over every node (p.mul_(0.); p.add_(new); d_sgd.py:29-35)."""
+    import copy
+    with torch.no_grad():
+        w = [1 / len(active) for _ in active]
+        center = copy.deepcopy(active[0]["model"])
+        for c in center.parameters():
+            c.mul_(0)
+        for n, wi in zip(active, w):
+            for c, q in zip(center.parameters(), n["model"].parameters()):
+                c.add_(wi * q)
+        for n in all_nodes:
+            for q, c in zip(n["model"].parameters(), center.parameters()):
+                q.mul_(0.)
+                q.add_(c)
+
+
+def test_sample_average_bitwise(gpu, monkeypatch):
+    """niidmix.d_sgd.sample_average (the slab-level 'sample' round: average of the active rows,
+    then update_models of EVERY row on the GPU) == the reference's CPU arithmetic, bit for bit,
+    with inf / NaN / -0.0 in the models (a non-finite row becomes NaN, zero sign rules) and the
+    slab streamed in several column windows."""
+    monkeypatch.setenv("NIIDMIX_WINDOW", "256")
+    from niidmix import d_sgd
+    torch.manual_seed(4)
+
+    def make():
+        torch.manual_seed(4)
+        nodes = [{"rank": r, "model": torch.nn.Linear(60, 9)} for r in range(23)]
+        with torch.no_grad():
+            nodes[3]["model"].weight[0, 0] = float("inf")
+            nodes[5]["model"].weight[1, 1] = float("nan")
+            nodes[7]["model"].bias[2] = -0.0
+            for n in nodes:
+                n["model"].bias[4] = 0.0 if n["rank"] % 2 else -0.0
+        return nodes
+    a, b = make(), make()
+    for pick in ([0, 4, 9, 17], [3, 1], [22, 7, 5, 0, 11]):
+        d_sgd.sample_average(a, [a[i] for i in pick])
+        _ref_sample_round(b, [b[i] for i in pick])
+        for u, v in zip(_params_of(a), _params_of(b)):
+            assert np.array_equal(np.isnan(u), np.isnan(v))
+            m = ~np.isnan(v)
+            assert np.array_equal(u[m].view(np.uint32), v[m].view(np.uint32))
+
+
+def test_sample_topology_training_rounds(gpu):
+    """Whole 'sample' topology rounds through niidmix.d_sgd.next_step (random-with-overlap
+    sampling, local SGD on CPU, the GPU average + broadcast) equal the same rounds with the
+    reference's CPU branch, bit for bit."""
+    from niidmix import d_sgd
+
+    def run(mode):
+        torch.manual_seed(1337)
+        d_sgd._sample_cache.clear()
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
+                  "topology": {"name": "sample", "sample-method": "random-with-overlap",
+                               "sample-size": 3, "sample-overlap": 1},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 20,
+                                "initial-averaging": False, "clique-gradient": False,
+                                "unbiased-gradient": False}}
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc = torch.nn.Linear(784, 10)
+
+            def forward(self, x, params):
+                return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+        g = torch.Generator().manual_seed(9)
+        data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+                for _ in range(600)]
+        nodes = []
+        for r in range(6):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 100:(r + 1) * 100],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        orig = d_sgd.sample_average
+        if mode == "cpu":
+            d_sgd.sample_average = _ref_sample_round
+        try:
+            state, _, _ = d_sgd.init(nodes, {"edges": {}, "weights": torch.tensor([])}, params)
+            for _ in range(5):
+                state, losses, done, active = d_sgd.next_step(state, params, None)
+        finally:
+            d_sgd.sample_average = orig
+        return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
+                for n in nodes]
+
+    for u, v in zip(run("gpu"), run("cpu")):
+        assert torch.equal(u, v)

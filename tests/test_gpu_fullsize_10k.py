@@ -1,0 +1,133 @@
+"""Parity at BASELINE.json configs[4]'s sizes (10 000-node d-cliques, P = 2^20), through the same
+layouts and launch paths as bench.py --config dcliques10000 and the multi-GPU stripes:
+
+  * the single-GPU fast round exactly as benched: relabeled (clique-contiguous) rows, column-blocked
+    VMM slabs [4096, 10000, 256] (block width 256: a clique gathers 99 gateway rows, > 64), the
+    clique kernel; blocks 0, 2047 and 4095 against the oracle (block 4095 starts 1.05e10 elements
+    into the slab: past 2^31, 2^32 and 2^33), plus column-sum preservation over every block;
+  * the exact default (tile-lds-exact, 199 staged rows per clique -> 96-column items) on row-major
+    [10000, 2^20] slabs, bitwise on windows that straddle item boundaries, the ragged last item and
+    rows whose offsets exceed 2^33 elements;
+  * one rank of the 8000-node weak N=8 column-stripe shape (StripedMixer: 79 gateway terms per
+    clique, B = 256), windows against the oracle and column sums over the whole stripe.
+
+Columns of Θ' = Wᵀ Θ are independent (d_sgd.py:96-116 mixes every tensor element-wise), so a column
+window of the oracle is the full computation restricted to those columns.  Reference topology:
+random_cliques.py:43-44 (fully-connected interclique by default), interclique.py:57-75.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+P_FULL = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def dc10k():
+    from niidmix.generate import dcliques_csr
+    return dcliques_csr(10000, 100, "fully-connected", 1337)
+
+
+def _free():
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _check_fast(oracle_mod, csr, xw, yw, what):
+    ref = oracle_mod.mix_exact_c(xw, csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xw, csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(yw, ref, bound, rtol=RTOL)
+    assert ok, (what, worst)
+
+
+def _blocked_colsum_gap(xb, yb):
+    """max |colsum(x) - colsum(y)| over every column of two [K, N, B] slabs (fp64 sums)."""
+    gap = 0.0
+    for k0 in range(0, xb.shape[0], 256):
+        sx = torch.sum(xb[k0:k0 + 256], dim=1, dtype=torch.float64)
+        sy = torch.sum(yb[k0:k0 + 256], dim=1, dtype=torch.float64)
+        gap = max(gap, torch.max(torch.abs(sx - sy)).item())
+    return gap
+
+
+def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod):
+    from niidmix import memory, ops
+    csr, cliques = dc10k
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.kernel_for("fast") == "clique" and m.plan.max_clique_res == 99
+    perm, bc = m.device_layout()
+    assert perm is not None and bc == 256
+    m = m.relabeled(perm)
+    xb = memory.empty_blocked(10000, P_FULL, gpu, bc)
+    assert tuple(xb.shape) == (4096, 10000, 256)
+    xb.normal_(generator=torch.Generator(device=gpu).manual_seed(10))
+    yb = memory.empty_blocked(10000, P_FULL, gpu, bc)
+    yb.fill_(float("nan"))                       # every output element must be written
+    m.mix_blocked(xb, yb, P_FULL)
+    torch.cuda.synchronize()
+    assert 4095 * xb.stride(0) > (1 << 33)
+    for k in (0, 2047, 4095):
+        _check_fast(oracle_mod, m.csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
+    assert not torch.isnan(yb).any().item()
+    assert _blocked_colsum_gap(xb, yb) < 2e-3
+    del xb, yb
+    _free()
+
+
+def test_dcliques10000_tile_lds_exact_rowmajor(dc10k, gpu, oracle_mod):
+    from niidmix import memory, ops
+    csr, cliques = dc10k
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.kernel_for("exact") == "tile-lds-exact"
+    assert m.tlds.max_src == 199
+    x = memory.empty_slab(10000, P_FULL, gpu)
+    x.normal_(generator=torch.Generator(device=gpu).manual_seed(11))
+    y = memory.empty_slab(10000, P_FULL, gpu)
+    y.fill_(float("nan"))
+    m(x, out=y, mode="exact")
+    torch.cuda.synchronize()
+    # 96-column items (199 rows x 96 cols x 4 B = 76 KB: two blocks per CU); P = 2^20 = 10922 x 96
+    # + 64, so the last item is ragged
+    w = 96 * 3
+    for c0 in (0, 96 * 5461 - 40, P_FULL - w):
+        xw = x[:, c0:c0 + w].cpu().numpy()
+        ref = oracle_mod.mix_exact_c(xw, csr.row_ptr, csr.col, csr.val)
+        assert oracle_mod.bitwise_equal(y[:, c0:c0 + w].cpu().numpy(), ref), c0
+    # every element written; column sums preserved over ALL columns
+    assert not torch.isnan(y).any().item()
+    sx = torch.zeros(P_FULL, dtype=torch.float64, device=gpu)
+    sy = torch.zeros(P_FULL, dtype=torch.float64, device=gpu)
+    for r0 in range(0, 10000, 1000):
+        sx += torch.sum(x[r0:r0 + 1000], dim=0, dtype=torch.float64)
+        sy += torch.sum(y[r0:r0 + 1000], dim=0, dtype=torch.float64)
+    assert torch.max(torch.abs(sx - sy)).item() < 2e-3
+    del x, y
+    _free()
+
+
+def test_dcliques8000_stripe_rank7(gpu, oracle_mod):
+    """Weak-scaling N=8's per-rank shape: 8000 nodes (80 cliques, 79 gateway terms each, B = 256),
+    rank 7's column stripe [917504, 1048576) of P = 2^20 through StripedMixer."""
+    from niidmix.shard import StripedMixer
+    sm = StripedMixer.dcliques(8000, 100, world=8, rank=7, interclique="fully-connected",
+                               device=gpu, p=P_FULL)
+    assert sm.blocked and sm.block_cols == 256 and sm.mixer.plan.max_clique_res == 79
+    assert (sm.c0, sm.c1) == (7 * (P_FULL // 8), P_FULL)
+    x = torch.randn(8000, sm.p_local, device=gpu, generator=torch.Generator(device=gpu).manual_seed(12))
+    xb, yb = sm.to_layout(x), sm.empty()
+    sm(xb, yb)
+    y = sm.from_layout(yb)
+    torch.cuda.synchronize()
+    # the rank-order CSR (the stripe mixer runs the relabeled one)
+    from niidmix.generate import dcliques_csr
+    csr, _ = dcliques_csr(8000, 100, "fully-connected", 1337)
+    w = 512
+    for c0 in (0, sm.p_local // 2 - 200, sm.p_local - w):
+        _check_fast(oracle_mod, csr, x[:, c0:c0 + w].cpu().numpy(), y[:, c0:c0 + w].cpu().numpy(), c0)
+    gap = torch.max(torch.abs(torch.sum(x, 0, dtype=torch.float64) -
+                              torch.sum(y, 0, dtype=torch.float64))).item()
+    assert gap < 2e-3
+    del x, xb, yb, y
+    _free()

@@ -440,3 +440,69 @@ def test_bigclique_blocked_layout(n, size, inter, gpu):
     oo = flat[k * rows * b // 2: k * rows * b // 2 + k * rows * b].view(k, rows, b)
     with pytest.raises(RuntimeError, match="overlap"):
         m.mix_blocked(xo, oo, p)
+
+
+@pytest.mark.parametrize("tile", ["8x13x4x13", "16x7x8x2", "16x7x4x7"])
+@pytest.mark.parametrize("name", golden_cases())
+def test_multi_clique_tile_vs_golden(name, tile, gpu, oracle_mod, monkeypatch):
+    """The multi-clique tile (k_mix_clique_q: 4 cliques x 64 columns per item, the default for
+    >= 4096 member rows) forced on every golden clique case, non-finite fixtures included: row-major
+    slabs (64-bit row offsets) and column-blocked slabs of 64 and 256 columns (32-bit offsets),
+    within the tolerance, with the reference's inf / NaN pattern; blocked == row-major bitwise."""
+    from niidmix import memory
+    g = load_golden(name)
+    m = _mixer(g, gpu)
+    p = g["x"].shape[1]
+    if m.plan is None or p % 4 or m.plan.max_clique > 104:
+        pytest.skip("no clique plan / p % 4 / clique > 104 members")
+    monkeypatch.setenv("NIIDMIX_CLIQUE_Q", "4")
+    monkeypatch.setenv("NIIDMIX_CLIQUE_QT", tile)
+    if m.plan.max_clique > 112 or int(tile.split("x")[0]) * int(tile.split("x")[1]) < m.plan.max_clique:
+        pytest.skip("clique larger than the tile")
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="clique").cpu().numpy()
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+    assert ok, (name, tile, worst)
+    for bc in (64, 256):
+        yb = memory.empty_blocked(m.n, p, gpu, bc)
+        m.mix_blocked(memory.to_blocked(x, bc), yb, p)
+        assert oracle_mod.bitwise_equal(memory.from_blocked(yb, p).cpu().numpy(), y), (name, tile, bc)
+
+
+@pytest.mark.parametrize("n,inter", [(4000, "fully-connected"), (5000, "smallworld"), (4200, "ring")])
+def test_multi_clique_tile_auto(n, inter, gpu, oracle_mod, monkeypatch):
+    """Many cliques (>= 4096 member rows): the launcher picks the multi-clique tile by itself; a
+    ragged column tail (p = 4100) and a clique count not divisible by 4 (42 cliques of 100); equal
+    within the tolerance to the one-clique tile (NIIDMIX_CLIQUE_Q=1) and to the oracle."""
+    from niidmix import memory, ops
+    from niidmix.generate import dcliques_csr
+    csr, cliques = dcliques_csr(n, 100, inter, 1337)
+    m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
+    assert m.plan is not None, m.plan_reason
+    p = 4100
+    xh = torch.randn(n, p, generator=torch.Generator().manual_seed(n))
+    x = xh.to(gpu)
+    monkeypatch.delenv("NIIDMIX_CLIQUE_Q", raising=False)
+    monkeypatch.delenv("NIIDMIX_CLIQUE_QT", raising=False)
+    y = m(x, kernel="clique").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xh.numpy(), csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+    assert ok, worst
+    monkeypatch.setenv("NIIDMIX_CLIQUE_Q", "1")
+    y1 = m(x, kernel="clique").cpu().numpy()
+    ok, worst = oracle_mod.check_tolerance(y1, ref, bound, rtol=RTOL)
+    assert ok, worst
+    assert not np.array_equal(y, y1) or n < 4096    # the two tiles really differ (summation order)
+    monkeypatch.delenv("NIIDMIX_CLIQUE_Q")
+    perm, bc = m.device_layout()
+    mr = m.relabeled(perm)
+    pt = torch.from_numpy(perm).to(gpu)
+    xp = torch.empty_like(x)
+    xp[pt] = x
+    yb = memory.empty_blocked(n, p, gpu, bc)
+    mr.mix_blocked(memory.to_blocked(xp, bc), yb, p)
+    ok, worst = oracle_mod.check_tolerance(memory.from_blocked(yb, p)[pt].cpu().numpy(), ref, bound,
+                                           rtol=RTOL)
+    assert ok, worst

@@ -124,13 +124,56 @@ def test_randomized_topology_sparse_and_dense_files(tmp_path, monkeypatch):
                            "weights": "metropolis-hasting", "randomize": True}}
     t = d_sgd.randomized_topology(nodes, params, rd)
     ref, _ = generate.random_graph_csr(60, 6, 8)
-    assert np.array_equal(topology.to_csr(t).val, ref.val) and t["weights"] is None
+    assert np.array_equal(topology.to_csr(t).val, ref.val)
+    # the weights the reference's randomized round leaves in state['topology'] (d_sgd.py:233)
+    assert isinstance(t["weights"], torch.Tensor) and t["weights"].shape == (60, 60)
     dense = topology.to_csr(topology.load_file(os.path.join(rd, "topology.json")))
     np.testing.assert_array_equal(dense.col, ref.col)
     assert np.array_equal(dense.val.view(np.uint32), ref.val.view(np.uint32))
     monkeypatch.setattr(d_sgd, "DENSE_JSON_MAX", 10)
     time.sleep(0.01)
     params["topology"]["topology-seed"] = 9
-    d_sgd.randomized_topology(nodes, params, rd)            # sparse file only: newer than the JSON
-    got = topology.to_csr(topology.load(rd))
-    np.testing.assert_array_equal(got.col, generate.random_graph_csr(60, 6, 9)[0].col)
+    t9 = d_sgd.randomized_topology(nodes, params, rd)       # above the cap: a SPARSE topology.json
+    assert t9["weights"].numel() == 0
+    want = generate.random_graph_csr(60, 6, 9)[0]
+    for loaded in (topology.load(rd), topology.load_file(os.path.join(rd, "topology.json"))):
+        got = topology.to_csr(loaded)                        # the JSON never lags the graph
+        np.testing.assert_array_equal(got.col, want.col)
+        assert np.array_equal(got.val.view(np.uint32), want.val.view(np.uint32))
+
+
+def test_sparse_rundir_reads_with_reference_loader(tmp_path):
+    """niidmix.sparse_topology writes a topology.json the reference's own loader reads unchanged
+    (run.py:92-93 -> setup.topology.load, topology/__init__.py:4-12): the committed fixture is what
+    that loader returned for this very file (tests/golden/make_sparse_load.py).  The restated
+    loader (load_file) returns the same, and the plugin's to_csr turns it into the reference's
+    dense-W operator bit for bit (MH weights rebuilt from the edges, or the companion CSR)."""
+    import json
+    from niidmix import sparse_topology, topology
+    rd = _rundir(tmp_path, 300, 1337)
+    sparse_topology.main(["d-cliques", "--rundir", rd, "--max-clique-size", "30"])
+    text = (tmp_path / "topology.json").read_text()
+    assert json.loads(text) == json.loads(open(os.path.join(GOLDEN, "sparse_dcliques300.written.json")).read())
+    ref = json.loads(open(os.path.join(GOLDEN, "sparse_dcliques300.refload.json")).read())
+    t = topology.load_file(str(tmp_path / "topology.json"))
+    w = t["weights"]
+    assert [type(w).__name__, str(w.dtype), list(w.shape)] == \
+        [ref["weights_type"], ref["weights_dtype"], ref["weights_shape"]]
+    assert {str(k): v for k, v in t["edges"].items()} == ref["edges"]
+    assert all(isinstance(k, int) for k in t["edges"]) and ref["edge_key_types"] == ["int"]
+    assert t["cliques"] == ref["cliques"] and sorted(t) == ref["keys"]
+    g = load_golden("dcliques300_fc_p37")                   # the reference's dense-W round
+    for topo in (t, topology.load(rd)):
+        csr = topology.to_csr(topo)
+        np.testing.assert_array_equal(csr.row_ptr, g["row_ptr"])
+        np.testing.assert_array_equal(csr.col, g["col"])
+        assert np.array_equal(csr.val.view(np.uint32), g["val"].view(np.uint32))
+    assert "csr" in topology.load(rd) and "csr" not in t
+
+
+def test_sparse_weights_errors():
+    with pytest.raises(ValueError, match="weights-kind"):
+        T.to_csr({"edges": {0: [1], 1: [0]}, "weights": torch.tensor([])})
+    with pytest.raises(ValueError, match="every rank"):
+        T.to_csr({"edges": {0: [2], 2: [0]}, "weights": [], "weights-kind": T.SPARSE_KIND})
+    assert T.to_csr({"edges": {}, "weights": torch.tensor([])}).n == 0
