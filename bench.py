@@ -68,7 +68,8 @@ def parse():
                              "dcliques10000"])
     ap.add_argument("--p", type=int, default=None, help="parameters per node (default per config)")
     ap.add_argument("--kernel", default="auto",
-                    choices=["auto", "csr-exact", "csr-fast", "clique", "dense", "tile-exact", "tile-fast", "tile-lds-exact", "tile-lds-fast"])
+                    choices=["auto", "csr-exact", "csr-fast", "ell-exact", "ell-fast", "clique", "dense", "tile-exact",
+                             "tile-fast", "tile-lds-exact", "tile-lds-fast"])
     ap.add_argument("--interclique", default="fully-connected",
                     choices=["fully-connected", "smallworld", "ring"],
                     help="multi-GPU global d-cliques interclique topology")
@@ -105,8 +106,9 @@ def parse():
     ap.add_argument("--windows", type=int, default=8,
                     help="multi-GPU: column windows the halo exchange is pipelined over")
     ap.add_argument("--single-ref", default="auto", choices=["auto", "on", "off"],
-                    help="multi-GPU fixed problem (--config dcliques10000): rank 0 also times the "
-                         "whole problem on its own GPU and reports the speed-up (auto: on)")
+                    help="multi-GPU: rank 0 also times the N=1 point on its own GPU in the same run "
+                         "(--config dcliques10000: the whole fixed problem -> speedup_vs_1gpu; "
+                         "weak line: nodes_per_gpu nodes -> weak_efficiency_vs_1gpu) (auto: on)")
     return ap.parse_args()
 
 
@@ -239,6 +241,74 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
 
 def traffic_key(args, kernel, p, slab_layout):
     return f"{args.config}/{args.workload}/{kernel}/p{p}/{slab_layout}"
+
+
+def timed_rounds(step, xa, xb, steps, warmup, dev, dist=None, use_graph=False, backend="nccl"):
+    """The timed region (the driver's contract): `warmup` untimed rounds, then EXACTLY `steps`
+    rounds bracketed by a barrier + device synchronize on both sides; the region time and the
+    mean per-launch time (HIP events around every launch on the launch stream, or the replayed
+    hipGraph's region / steps) are max-reduced over ranks.  step(a, b, evs) runs one round a -> b
+    (ping-pong).  On a CPU device (gloo tests of this loop) host timers replace the HIP events.
+    Returns (region_s, launch_ms, graph)."""
+    cpu = dev.type == "cpu"
+    for _ in range(warmup):
+        step(xa, xb)
+        xa, xb = xb, xa
+    graph = None
+    if use_graph and not cpu:
+        # the K timed rounds as ONE hipGraph (ping-pong unrolled); replayed once in the timed region
+        graph = torch.cuda.CUDAGraph()
+        a, b = xa, xb
+        with torch.cuda.graph(graph):
+            for _ in range(steps):
+                step(a, b)
+                a, b = b, a
+        graph.replay()                                   # warm replay
+        torch.cuda.synchronize(dev)
+    if cpu:
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        launches = []
+        for _ in range(steps):
+            t1 = time.perf_counter()
+            step(xa, xb)
+            launches.append(time.perf_counter() - t1)
+            xa, xb = xb, xa
+        region_s = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        launch_ms = float(np.mean(launches)) * 1e3
+    else:
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t_start.record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            for i in range(steps):
+                step(xa, xb, ev[i])
+                xa, xb = xb, xa
+        t_end.record(stream)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        region_s = t_start.elapsed_time(t_end) / 1e3
+        if graph is not None:
+            launch_ms = region_s * 1e3 / steps           # kernels back to back inside the graph
+        else:
+            launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        tt = torch.tensor([region_s, launch_ms], dtype=torch.float64,
+                          device=dev if (backend == "nccl" and not cpu) else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        region_s, launch_ms = tt.tolist()
+    return region_s, launch_ms, graph
 
 
 def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
@@ -511,63 +581,25 @@ def main():
         else:
             mixer(a, b, kernel=kernel, mode=mode, events=evs)
 
-    for _ in range(args.warmup):
-        step(xa, xb)
-        xa, xb = xb, xa
     use_graph = world == 1 and (args.graph == "on" or
                                 (args.graph == "auto" and n_local * cols_local * 4 < (256 << 20)))
-    graph = None
-    if use_graph:
-        # the K timed rounds as ONE hipGraph (ping-pong unrolled); replayed once in the timed region
-        graph = torch.cuda.CUDAGraph()
-        a, b = xa, xb
-        with torch.cuda.graph(graph):
-            for _ in range(args.steps):
-                step(a, b)
-                a, b = b, a
-        graph.replay()                                   # warm replay
-        torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        for i in range(args.steps):
-            step(xa, xb, ev[i])
-            xa, xb = xb, xa
-    t_end.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    region_s = t_start.elapsed_time(t_end) / 1e3
-    if graph is not None:
-        launch_ms = region_s * 1e3 / args.steps       # kernels back to back inside the graph
-    else:
-        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist:
-        tt = torch.tensor([region_s, launch_ms], dtype=torch.float64,
-                          device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        region_s, launch_ms = tt.tolist()
+    region_s, launch_ms, graph = timed_rounds(step, xa, xb, args.steps, args.warmup, dev, dist,
+                                              use_graph, backend)
     step_s = region_s / args.steps
     value = n_total * p * 4 / step_s / 1e9
     slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}], "
                    f"{row_order} rows" if xa.dim() == 3 and (blocked or args.shard == "stripes") else
                    "window-blocked [K, rows_in, w]" if xa.dim() == 3 else "row-major [N, P]")
     single = None
-    if fixed and args.single_ref != "off":
-        # the same fixed problem on ONE GPU (rank 0's), same kernel and layout: the N=1 point of
-        # this strong-scaling line, measured in the same run; the other ranks wait
+    if world > 1 and args.single_ref != "off":
+        # the N=1 point of this line, measured in the same run on rank 0's GPU with the same
+        # kernel and layout (the other ranks wait): the fixed problem alone (strong scaling), or
+        # one GPU's share of the weak line (nodes_per_gpu nodes, the same P)
         del xa, xb
         torch.cuda.empty_cache()
         if rank == 0:
-            single = single_gpu_round_ms(n_total, p, args.interclique, dev, args.steps, args.warmup)
+            n1 = n_total if fixed else args.nodes_per_gpu
+            single = single_gpu_round_ms(n1, p, args.interclique, dev, args.steps, args.warmup)
         dist.barrier()
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
@@ -632,7 +664,11 @@ def main():
             out["config"]["halo_GB_send_rank0"] = round(mixer.send_bytes / 1e9, 3)
         if single is not None:
             out["config"]["single_gpu_ms"] = round(single, 4)
-            out["config"]["speedup_vs_1gpu"] = round(single / (step_s * 1e3), 3)
+            if fixed:
+                out["config"]["speedup_vs_1gpu"] = round(single / (step_s * 1e3), 3)
+            else:       # weak: each GPU's work equals the N=1 round's
+                out["config"]["single_gpu_nodes"] = args.nodes_per_gpu
+                out["config"]["weak_efficiency_vs_1gpu"] = round(single / (step_s * 1e3), 3)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -24,7 +24,9 @@
  *
  * ABI 3 (this header): n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
  * niidmix_grad_segment_mean_f32 and niidmix_grad_segment_mean_blocked_f32 (full extent checks);
- * niidmix_update_rows_f32 added (the 'sample' topology's broadcast); cliques of <= 112 members
+ * niidmix_update_rows_f32 added (the 'sample' topology's broadcast); niidmix_mix_ell_f32 added
+ * (low-degree graphs); niidmix_sharded_* / niidmix_mix_sharded_f32 added (sharded round over
+ * several GPUs of one process, RCCL); cliques of <= 112 members
  * accept 64-column blocks (the multi-clique tile).
  */
 #ifndef NIIDMIX_H
@@ -99,6 +101,16 @@ const char *niidmix_last_error(void);
 int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                         int64_t p, const int64_t *row_ptr, const int32_t *col, const float *val,
                         int mode, void *stream);
+
+/* The same round over an ELL layout of the same W^T rows, for low-degree graphs (ring, grid,
+ * random regular): row r's entries are ell_col / ell_val[r*k .. r*k + ell_len[r]) in the CSR's
+ * order (self first), padded to k entries (the padding is never read as a term).  k: 3, 5 or 8.
+ * The gathers depend on one descriptor load (no row_ptr step) and a wave streams several column
+ * chunks of its row.  mode as niidmix_mix_csr_f32 (EXACT / FAST, | NIIDMIX_FLAG_AVERAGE_ONLY);
+ * bit-identical to it in EXACT mode. */
+int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                        int64_t p, int k, const int32_t *ell_col, const float *ell_val,
+                        const int32_t *ell_len, int mode, void *stream);
 
 /* Clique-factored mixing (fast mode only).  For each member m of clique c:
  *   y_m = a_m * x_m + sum_{g < n_groups} c_{m,g} * S_{c,g} + sum_r res_val[r] * x[res_col[r]]
@@ -233,6 +245,15 @@ typedef struct niidmix_tile_lds_plan {
     const int32_t *grp_tile_ptr;
     const int32_t *grp_src_ptr;
     const int32_t *grp_src_rows;
+    /* optional (rt 16; NULL = the per-position loop): the positions cut into segments, runs read
+     * from consecutive LDS slots with immediate offsets (niidmix.tile.build_tile_segments):
+     *   seg_ptr [n_sub+1] int32 segments of each tile;  seg [n_seg * 8] int32 per segment: first
+     *   slot, length (| 1 << 30: one position for the generic path, word 7 its position index),
+     *   weight-select bits (2 words), skip bits (2 words), first skipped tile row, first position;
+     *   seg_w [n_sub * 2] fp32 the tile's two weights */
+    const int32_t *seg_ptr;
+    const int32_t *seg;
+    const float *seg_w;
 } niidmix_tile_lds_plan;
 
 int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
@@ -295,6 +316,48 @@ int niidmix_sgd_step_rows_f32(float *p, int64_t ld_p, const float *g, int64_t ld
  *   overlap is refused);  avg [p] (device, overlapping neither) */
 int niidmix_update_rows_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                             int64_t p, const float *avg, void *stream);
+
+/* Sharded round over several GPUs of ONE process (the simulator's own model: every node in one
+ * process, run.py:136), nodes sharded by whole cliques (niidmix.shard.ShardPlan), the rows other
+ * shards read exchanged every round, then each shard's rows mixed by niidmix_mix_csr_f32 over
+ * [local rows | halo rows] (the local CSR keeps every row's operand order: exact mode is bitwise
+ * the single-GPU round).  The handle holds one RCCL communicator per shard (ncclCommInitAll,
+ * created once per topology and device set; librccl.so.1 is loaded on first use).  When several
+ * shards share a device (tests, one-GPU boxes) the exchange is device-to-device copies instead.
+ * Shard s, row-major slabs with ld = p:
+ *   x [rows_in, p]: its n_local rows, then its halo rows;  y [n_local, p]
+ *   row_ptr / col / val: CSR of its n_local rows over the rows_in input rows (device)
+ *   peer[j], j < n_peers (host): the shards it exchanges with; it sends
+ *     send_rows[send_ptr[j] .. send_ptr[j+1]) (device local row indices, in that peer's halo order;
+ *     send_ptr host, send_ptr[0] may be > 0) through send_buf (device, [send_ptr[n_peers] -
+ *     send_ptr[0], p]) and receives recv_count[j] rows into halo rows recv_row[j] .. (host)
+ *   stream: the shard's HIP stream (on its device)
+ * Every shard's receive count must equal what the peer sends it (checked); the call enqueues
+ * pack -> exchange -> mix on every shard's stream and returns without waiting. */
+typedef struct niidmix_sharded niidmix_sharded;
+typedef struct niidmix_shard {
+    int32_t device;
+    int32_t n_peers;
+    int64_t n_local, rows_in;
+    float *x;
+    float *y;
+    const int64_t *row_ptr;
+    const int32_t *col;
+    const float *val;
+    const int32_t *peer;
+    const int64_t *send_ptr;
+    const int32_t *send_rows;
+    float *send_buf;
+    const int64_t *recv_row;
+    const int64_t *recv_count;
+    void *stream;
+} niidmix_shard;
+
+int niidmix_sharded_create(int n_shards, const int *devices, niidmix_sharded **out);
+int niidmix_sharded_destroy(niidmix_sharded *h);
+/* 1 when the handle exchanges by device-to-device copies (shards sharing a device), 0 for RCCL. */
+int niidmix_sharded_is_loopback(const niidmix_sharded *h);
+int niidmix_mix_sharded_f32(niidmix_sharded *h, const niidmix_shard *shards, int64_t p, int mode);
 
 /* Device memory for node-state slabs, with the signatures of a PyTorch pluggable allocator
  * (torch.cuda.memory.CUDAPluggableAllocator; niidmix.memory.slab_pool uses them for a MemPool).

@@ -25,7 +25,9 @@
 //   k_mix_dense            Y = W^T X on v_mfma_f32_32x32x2_f32 (fp32 matrix cores), 128x128 tiles.
 //   k_mean_cols / k_row_dist2   uniform average + squared distance to it (consensus distance).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <dlfcn.h>
 #include <stdarg.h>
 #include <stdlib.h>
 #include <stdint.h>
@@ -258,6 +260,81 @@ __global__ __launch_bounds__(256) void k_mix_csr(const float *__restrict__ x, in
 #pragma unroll
         for (int q = 0; q < S; ++q)
             if (ok[q]) stv_nt<VW>(dst + cs[q], o + q * VW);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Low-degree mixing over an ELL descriptor layout (ring, grid: every row lists <= K entries).  The
+// CSR kernel's item is a chain row_ptr -> (col, val) -> gathers -> store per 256..512 columns; on a
+// LeNet-size ring (100 rows x 62 006 columns, 3 entries) that chain, not the bytes, set the time.
+// Here row r's entries sit at r*K + j (ell_col / ell_val, ell_len[r] of them, self first), so the
+// gathers depend on ONE descriptor load, and a wave walks CH consecutive 256-column chunks of
+// its row with all their gathers in flight together (descriptors amortised over CH chunks).
+// Arithmetic as k_mix_csr (exact: fl(acc + fl(w*x)) in list order on top of x_self*0; fast: fma).
+// Work order is XCD-aware: the rows of one column slice run on one XCD, so a source row gathered by
+// its ~K readers is read from HBM once.
+template <bool EXACT, int VW, int K, int CH>
+__global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, int64_t ld_x,
+                                                 float *__restrict__ y, int64_t ld_y, int64_t n_rows,
+                                                 int64_t p, const int32_t *__restrict__ ell_col,
+                                                 const float *__restrict__ ell_val,
+                                                 const int32_t *__restrict__ ell_len,
+                                                 int64_t n_row_groups, int64_t n_items, int avg_only) {
+    constexpr int S = 4 / VW;                 // slots per lane per chunk
+    constexpr int NE = 4;                     // columns per lane per chunk
+    constexpr int64_t CW = 64 * NE;           // columns per chunk (256)
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t t = blockIdx.x;
+    if (t >= n_items) return;
+    const int64_t xcd = t & 7, local = t >> 3;
+    const int64_t slice = (local / n_row_groups) * 8 + xcd;
+    const int64_t row = (local % n_row_groups) * 4 + wave;
+    const int64_t c_beg = slice * CH * CW;
+    if (row >= n_rows || c_beg >= p) return;  // wave-uniform
+    const int li = lane < K ? lane : K - 1;
+    const int d_col = ell_col[row * K + li];
+    const float d_val = ell_val[row * K + li];
+    const int len = __builtin_amdgcn_readfirstlane(ell_len[row]);
+    // gathers of every chunk of the slice, all in flight before the first use
+    float xv[CH][K][NE];
+    int64_t cs[CH][S];
+    bool ok[CH][S];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const int64_t cq = c_beg + c * CW + VW * lane + 64 * VW * q;
+            ok[c][q] = cq < p;                // p % VW == 0: a slot is all-in or all-out
+            cs[c][q] = ok[c][q] ? cq : 0;
+        }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const float *src = x + (int64_t)__builtin_amdgcn_readlane(d_col, j < len ? j : 0) * ld_x;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int q = 0; q < S; ++q) ldv<VW>(src + cs[c][q], xv[c][j] + q * VW);
+    }
+    float *dst = y + row * ld_y;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        float z[NE], acc[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) { z[e] = xv[c][0][e] * 0.f; acc[e] = z[e]; }   // self * 0
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (j < len) {                                                            // wave-uniform
+                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_val), j));
+#pragma unroll
+                for (int e = 0; e < NE; ++e) acc[e] = axpy<EXACT>(w, xv[c][j][e], acc[e]);
+            }
+        float o[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+            if (ok[c][q]) stv_nt<VW>(dst + cs[c][q], o + q * VW);
     }
 }
 
@@ -1490,7 +1567,7 @@ static_assert(sizeof(TileAcc<32>) == 64 * sizeof(float), "two halves of 16 pairs
                  : [stop] "s"(stop), [last] "s"(last), [vm] "v"(v_meta), [vw] "v"(v_w),             \
                    [l8] "v"(lane8)                                                                  \
                  : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74",     \
-                   "v75", "v76", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "scc",     \
+                   "v75", "v76", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "m0", "scc", \
                    "memory")
 typedef TileAcc<16>::V Acc16;
 template <bool EXACT>
@@ -1499,6 +1576,132 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     const int last = stop - 1;
     if constexpr (EXACT) NIIDMIX_TLDS_RUN(NIIDMIX_UPD_EXACT);
     else NIIDMIX_TLDS_RUN(NIIDMIX_UPD_FAST);
+}
+
+// The RT = 16 position loop over one SEGMENT (niidmix.tile.build_tile_segments): positions
+// i = 0 .. len-1 read consecutive LDS slots, so position i's row sits at one base address +
+// i * RB bytes -- an immediate offset, no per-position descriptor, no v_readlane; its weight is the
+// tile's w0 or w1 (bit i of wsel, picked by SALU) and it is taken by every row, or (bit i of skip)
+// by all rows but the next one of the segment's skipped rows r0, r0 + 1, ... (saved, updated with
+// the others, restored: bit-exact).  The row two positions ahead is read while one is applied;
+// the segment's LDS allocation holds two spare rows for the reads past its end.
+// Scratch registers are asm operands (compiler-allocated), not fixed ones, so that the values the
+// kernel keeps live across the segment loop can share the low VGPRs: x0..x3 the rotating row pairs,
+// pr the product, sv0/sv1 the saved skipped row, va the read address.
+#define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
+#define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
+    "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
+    "s_bitcmp1_b32 %[wsel], s47\n\t"                                                                 \
+    "s_cselect_b32 s44, %[w1], %[w0]\n\t"                                                            \
+    "s_bitcmp1_b32 %[skip], s47\n\t"                                                                 \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                       \
+    "s_cbranch_scc1 .Lseg_skip" K "_%=\n\t" UPD(XD)                                                 \
+    "\n.Lseg_back" K "_%=:\n\t"                                                                     \
+    "s_add_u32 s47, s47, 1\n\t"                                                                      \
+    "s_cmp_ge_u32 s47, %[len]\n\t"                                                                   \
+    "s_cbranch_scc1 .Lseg_done_%=\n\t"
+#define NIIDMIX_SEG_SKIPBLK(XD, K, UPD)                                                              \
+    "\n.Lseg_skip" K "_%=:\n\t"                                                                     \
+    "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
+    "v_mov_b32 %[sv0], v32\n\t"                                                                      \
+    "v_mov_b32 %[sv1], v33\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t" UPD(XD)                                                                  \
+    "s_set_gpr_idx_on s46, gpr_idx(DST)\n\t"                                                        \
+    "v_mov_b32 v32, %[sv0]\n\t"                                                                      \
+    "v_mov_b32 v33, %[sv1]\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                          \
+    "s_add_u32 s46, s46, 2\n\t"                                                                      \
+    "s_branch .Lseg_back" K "_%=\n\t"
+#define NIIDMIX_SEG_RUN(UPD)                                                                         \
+    asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"                                             \
+                 "ds_read_b64 %[x0], %[va]\n\t"                                                     \
+                 "ds_read_b64 %[x1], %[va] offset:%[o1]\n\t"                                        \
+                 "s_mov_b32 s47, 0\n\t"                                                              \
+                 "s_lshl_b32 s46, %[r0], 1\n"                                                        \
+                 ".Lseg_loop_%=:\n\t"                                                                \
+                 NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", "0", UPD)                                    \
+                 NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", "1", UPD)                                    \
+                 NIIDMIX_SEG_POS("%[x2]", "%[x0]", "o4", "2", UPD)                                    \
+                 NIIDMIX_SEG_POS("%[x3]", "%[x1]", "o5", "3", UPD)                                    \
+                 "v_add_u32 %[va], %[o4], %[va]\n\t"                                                 \
+                 "s_branch .Lseg_loop_%=\n\t"                                                        \
+                 NIIDMIX_SEG_SKIPBLK("%[x0]", "0", UPD)                                               \
+                 NIIDMIX_SEG_SKIPBLK("%[x1]", "1", UPD)                                               \
+                 NIIDMIX_SEG_SKIPBLK("%[x2]", "2", UPD)                                               \
+                 NIIDMIX_SEG_SKIPBLK("%[x3]", "3", UPD)                                               \
+                 "\n.Lseg_done_%=:\n\t"                                                             \
+                 "s_waitcnt lgkmcnt(0)"                                                              \
+                 : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2),             \
+                   [x3] "=&v"(x3), [pr] "=&v"(pr), [sv0] "=&v"(sv0), [sv1] "=&v"(sv1),              \
+                   [va] "=&v"(va)                                                                   \
+                 : [addr] "s"(addr), [len] "s"(len), [wsel] "s"(wsel), [skip] "s"(skip),             \
+                   [r0] "s"(r0), [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),            \
+                   [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB)             \
+                 : "s44", "s45", "s46", "s47", "m0", "scc", "memory")
+template <bool EXACT, int RB>
+__device__ __forceinline__ void tlds16_seg(Acc16 &acc, int addr, int len, uint32_t wsel,
+                                           uint32_t skip, int r0, int w0, int w1, int lane8) {
+    static_assert(5 * RB < 65536, "ds_read immediate offset");
+    uint64_t x0, x1, x2, x3, pr;
+    uint32_t sv0, sv1, va;
+    if constexpr (EXACT) NIIDMIX_SEG_RUN(NIIDMIX_SEG_UPD_EXACT);
+    else NIIDMIX_SEG_RUN(NIIDMIX_UPD_FAST);
+    (void)pr;
+}
+
+// One position taken by the rows of `mask` with the uniform weight w (a segment's MASKED entry: a
+// row taking a gateway's inter-clique edge alone, a source two rows order differently, or one
+// weight class of a position whose rows carry different weights -- split by weight, each row still
+// takes it once, in its own order).  Each row is reached by GPR-index mode (s_set_gpr_idx), the
+// accumulator tuple stays pinned in v[32:63].
+template <bool EXACT>
+__device__ __forceinline__ void tlds16_masked(Acc16 &acc, int addr, uint32_t mask, int w, int lane8) {
+    uint32_t x0, x1, va, m;
+    if constexpr (EXACT) {
+        asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"
+                     "ds_read_b32 %[x0], %[va]\n\t"
+                     "ds_read_b32 %[x1], %[va] offset:4\n\t"
+                     "s_mov_b32 %[m], %[mask]\n\t"
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "v_mul_f32 %[x0], %[w], %[x0]\n\t"
+                     "v_mul_f32 %[x1], %[w], %[x1]\n"
+                     ".Lmsk_loop_%=:\n\t"
+                     "s_ff1_i32_b32 s46, %[m]\n\t"
+                     "s_cmp_lt_i32 s46, 0\n\t"
+                     "s_cbranch_scc1 .Lmsk_done_%=\n\t"
+                     "s_bitset0_b32 %[m], s46\n\t"
+                     "s_lshl_b32 s46, s46, 1\n\t"
+                     "s_set_gpr_idx_on s46, gpr_idx(SRC0,DST)\n\t"
+                     "v_add_f32 v32, v32, %[x0]\n\t"
+                     "v_add_f32 v33, v33, %[x1]\n\t"
+                     "s_set_gpr_idx_off\n\t"
+                     "s_branch .Lmsk_loop_%=\n"
+                     ".Lmsk_done_%=:"
+                     : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [va] "=&v"(va), [m] "=&s"(m)
+                     : [addr] "s"(addr), [mask] "s"(mask), [w] "s"(w), [l8] "v"(lane8)
+                     : "s46", "m0", "scc", "memory");
+    } else {
+        asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"
+                     "ds_read_b32 %[x0], %[va]\n\t"
+                     "ds_read_b32 %[x1], %[va] offset:4\n\t"
+                     "s_mov_b32 %[m], %[mask]\n\t"
+                     "s_waitcnt lgkmcnt(0)\n"
+                     ".Lmsk_loop_%=:\n\t"
+                     "s_ff1_i32_b32 s46, %[m]\n\t"
+                     "s_cmp_lt_i32 s46, 0\n\t"
+                     "s_cbranch_scc1 .Lmsk_done_%=\n\t"
+                     "s_bitset0_b32 %[m], s46\n\t"
+                     "s_lshl_b32 s46, s46, 1\n\t"
+                     "s_set_gpr_idx_on s46, gpr_idx(SRC2,DST)\n\t"
+                     "v_fma_f32 v32, %[x0], %[w], v32\n\t"
+                     "v_fma_f32 v33, %[x1], %[w], v33\n\t"
+                     "s_set_gpr_idx_off\n\t"
+                     "s_branch .Lmsk_loop_%=\n"
+                     ".Lmsk_done_%=:"
+                     : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [va] "=&v"(va), [m] "=&s"(m)
+                     : [addr] "s"(addr), [mask] "s"(mask), [w] "s"(w), [l8] "v"(lane8)
+                     : "s46", "m0", "scc", "memory");
+    }
 }
 
 // Apply op(acc_row, r) to the rows of the wave-uniform mask m.  No per-row select: on gfx950 a lane
@@ -1541,14 +1744,16 @@ __device__ __forceinline__ void apply_mask(TileAcc<RT> &acc, uint32_t m, Op op) 
 #endif
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
-template <bool EXACT, int RT, int SV, int RS>
+template <bool EXACT, int RT, int SV, int RS, bool SEG>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
     const int32_t *__restrict__ grp_src_rows, const int64_t *__restrict__ sub_ptr,
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
-    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only) {
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
+    const int32_t *__restrict__ seg_ptr, const int32_t *__restrict__ seg,
+    const float *__restrict__ seg_w) {
     // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
     // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
@@ -1618,6 +1823,36 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
             acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
         }
+        if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && NIIDMIX_TLDS_SPLIT == 0) {
+            {                                                            // segment loop (tile.py)
+                const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
+                const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
+                for (int sb = sb0; sb < sb1; sb += 64) {
+                    // 64 segments' descriptors lane-parallel (one int4 each), handed out by
+                    // v_readlane: a run: x = first slot | length << 12 | first skipped row << 20,
+                    // y = weight-select bits, z = skip bits; a MASKED position: x = slot | 1 << 30,
+                    // y = the rows that take it, z = its weight (fp32 bits)
+                    const int cnt = sb1 - sb < 64 ? sb1 - sb : 64;
+                    const int4 da = reinterpret_cast<const int4 *>(seg)[sb + (lane < cnt ? lane : cnt - 1)];
+                    for (int j = 0; j < cnt; ++j) {
+                        const int hd = __builtin_amdgcn_readlane(da.x, j);
+                        if (hd & (1 << 30)) {                            // one MASKED position
+                            tlds16_masked<EXACT>(acc.v[0], (int)lds_base + (hd & 0xfff) * rs * (int)sizeof(f2),
+                                                 (uint32_t)__builtin_amdgcn_readlane(da.y, j),
+                                                 __builtin_amdgcn_readlane(da.z, j), lane8);
+                            continue;
+                        }
+                        const int s0 = hd & 0xfff, ln = (hd >> 12) & 0xff, r0 = (hd >> 20) & 0xff;
+                        const uint32_t wsel = (uint32_t)__builtin_amdgcn_readlane(da.y, j);
+                        const uint32_t skp = (uint32_t)__builtin_amdgcn_readlane(da.z, j);
+                        tlds16_seg<EXACT, rs * (int)sizeof(f2)>(acc.v[0], (int)lds_base + s0 * rs * (int)sizeof(f2),
+                                                               ln, wsel, skp, r0, w0, w1, lane8);
+                    }
+                }
+                goto tile_epilogue;
+            }
+        }
+        {
         const bool pad_slot = __builtin_amdgcn_readlane(d_row, RT - 1) < 0;   // slot RT-1 unused
         const int64_t beg = sub_ptr[sub], end = sub_ptr[sub + 1];
         for (int64_t kb = beg; NIIDMIX_TLDS_SPLIT != 1 && kb < end; kb += 64) {
@@ -1791,6 +2026,8 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 for (int u = 0; u < D; ++u) xa[u] = xb[u];
             }
         }
+        }
+    tile_epilogue:
         // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc)
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
@@ -1982,6 +2219,61 @@ __global__ __launch_bounds__(256) void k_sgd_step_rows(float *__restrict__ p, in
     }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Halo pack of the sharded round: out[i, :] = x[rows[i], :] (the rows a peer shard reads), so that
+// one contiguous send per peer carries them.
+template <int V>
+__global__ __launch_bounds__(256) void k_gather_rows(const float *__restrict__ x, int64_t ld_x,
+                                                     const int32_t *__restrict__ rows, int64_t n_rows,
+                                                     int64_t p, float *__restrict__ out, int64_t ld_o,
+                                                     int64_t n_chunks) {
+    for (int64_t t = blockIdx.x; t < n_rows * n_chunks; t += gridDim.x) {
+        const int64_t i = t / n_chunks;
+        const int64_t c = (t % n_chunks) * (256 * V) + (int64_t)threadIdx.x * V;
+        if (c >= p) continue;
+        float v[V];
+        ldv<V>(x + (int64_t)rows[i] * ld_x + c, v);
+        if constexpr (V == 4) *reinterpret_cast<float4 *>(out + i * ld_o + c) = make_float4(v[0], v[1], v[2], v[3]);
+        else out[i * ld_o + c] = v[0];
+    }
+}
+
+// RCCL, loaded on first use by niidmix_sharded_create (torch has usually loaded the same
+// librccl.so.1 already; dlopen then returns it): the library itself never depends on it.
+struct RcclApi {
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) error = nullptr;
+};
+
+const RcclApi *rccl_api() {
+    static RcclApi api;
+    static bool tried = false, ok = false;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!tried) {
+        tried = true;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            api.init_all = reinterpret_cast<decltype(api.init_all)>(dlsym(h, "ncclCommInitAll"));
+            api.destroy = reinterpret_cast<decltype(api.destroy)>(dlsym(h, "ncclCommDestroy"));
+            api.group_start = reinterpret_cast<decltype(api.group_start)>(dlsym(h, "ncclGroupStart"));
+            api.group_end = reinterpret_cast<decltype(api.group_end)>(dlsym(h, "ncclGroupEnd"));
+            api.send = reinterpret_cast<decltype(api.send)>(dlsym(h, "ncclSend"));
+            api.recv = reinterpret_cast<decltype(api.recv)>(dlsym(h, "ncclRecv"));
+            api.error = reinterpret_cast<decltype(api.error)>(dlsym(h, "ncclGetErrorString"));
+            ok = api.init_all && api.destroy && api.group_start && api.group_end && api.send &&
+                 api.recv && api.error;
+        }
+    }
+    return ok ? &api : nullptr;
+}
+
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int64_t grid_for(int64_t items) { return items < kMaxGrid ? ((items + 7) / 8) * 8 : kMaxGrid; }
@@ -2158,6 +2450,14 @@ void hbm_release(void *va, HbmBlock &b, size_t mapped) {
 }
 
 }  // namespace
+
+struct niidmix_sharded {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<ncclComm_t> comm;      // RCCL: one communicator per shard (rank = shard index)
+    bool loopback = false;             // several shards share a device: device-to-device copies
+    std::vector<hipEvent_t> ev_pack, ev_copy;
+};
 
 extern "C" {
 
@@ -2434,6 +2734,47 @@ int niidmix_mix_clique_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y,
     return launch_clique_tiled(x, ld_x, y, ld_y, p, plan, vec4, s);
 }
 
+int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                        int64_t p, int k, const int32_t *ell_col, const float *ell_val,
+                        const int32_t *ell_len, int mode, void *stream) {
+    if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE);
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (k < 1 || k > 8) return set_error(NIIDMIX_EUNSUPPORTED, "ELL width %d (1..8 supported)", k);
+    if (n_rows == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !ell_col || !ell_val || !ell_len) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    const int vw = (p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && (align & 15) == 0) ? 4
+                 : (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
+    // ELL width rounded up to an instantiated one; chunks in flight per wave by width (48 / 40 / 32
+    // gather VGPRs).  NIIDMIX_ELL_CH overrides the chunks (tuning).
+    const int kk = k <= 3 ? 3 : k <= 5 ? 5 : 8;
+    int ch = kk == 3 ? 4 : kk == 5 ? 2 : 1;
+    if (const char *e = getenv("NIIDMIX_ELL_CH")) { const int v = atoi(e); if (v == 1 || v == 2 || v == 4) ch = v; }
+    if (kk != k) return set_error(NIIDMIX_EINVAL, "ELL width %d: pad the rows to %d entries (ell_len keeps the lengths)", k, kk);
+    const int64_t n_slices = (p + 256 * ch - 1) / (256 * ch);
+    const int64_t n_row_groups = (n_rows + 3) / 4;
+    const int64_t n_items = n_row_groups * ((n_slices + 7) / 8) * 8;
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (rows, slice) items");
+    const dim3 grid((unsigned)n_items), block(256);
+#define NIIDMIX_ELL(E, V, KK, C) hipLaunchKernelGGL((k_mix_ell<E, V, KK, C>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, ell_col, ell_val, ell_len, n_row_groups, n_items, avg_only)
+#define NIIDMIX_ELL_C(E, V, KK) do { if (ch == 4) NIIDMIX_ELL(E, V, KK, 4); else if (ch == 2) NIIDMIX_ELL(E, V, KK, 2); else NIIDMIX_ELL(E, V, KK, 1); } while (0)
+#define NIIDMIX_ELL_K(E, V) do { if (kk == 3) NIIDMIX_ELL_C(E, V, 3); else if (kk == 5) NIIDMIX_ELL_C(E, V, 5); else NIIDMIX_ELL_C(E, V, 8); } while (0)
+#define NIIDMIX_ELL_V(E) do { if (vw == 4) NIIDMIX_ELL_K(E, 4); else if (vw == 2) NIIDMIX_ELL_K(E, 2); else NIIDMIX_ELL_K(E, 1); } while (0)
+    if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_ELL_V(true); else NIIDMIX_ELL_V(false);
+#undef NIIDMIX_ELL_V
+#undef NIIDMIX_ELL_K
+#undef NIIDMIX_ELL_C
+#undef NIIDMIX_ELL
+    return check_launch("k_mix_ell");
+}
+
 int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                          int64_t p, const niidmix_tile_plan *plan, int mode, void *stream) {
     if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
@@ -2515,9 +2856,13 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     // instead of one.  124 and 112 columns measured slower than 120.
     int cw = 128;
     const size_t lds_cu = 160 * 1024;
+    // segment loop (RT 16, plan->seg_ptr set): two spare staged rows for its reads past a segment
+    const bool seg = plan->rt == 16 && plan->seg_ptr != nullptr;
+    if (seg && (!plan->seg || !plan->seg_w)) return set_error(NIIDMIX_EINVAL, "null segment arrays");
+    const int stage_rows = plan->max_src + (seg ? 2 : 0);
     if (plan->rt == 16) {
         auto blocks = [&](int c) {
-            const size_t per = (size_t)plan->max_src * c * sizeof(float);
+            const size_t per = (size_t)stage_rows * c * sizeof(float);
             const size_t b = per ? lds_cu / per : 3;
             return (int)(b < 3 ? b : 3);
         };
@@ -2532,13 +2877,14 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const int64_t n_chunks = (p + cw - 1) / cw;
     const int64_t n_items = (int64_t)plan->n_grp * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
-    const size_t lds = (size_t)plan->max_src * cw * sizeof(float);
+    const size_t lds = (size_t)stage_rows * cw * sizeof(float);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = cw == 120 ? k_mix_tile_lds<E, R, V, 60> : cw == 96 ? k_mix_tile_lds<E, R, V, 48> : k_mix_tile_lds<E, R, V, 64>; \
+        auto kfn = seg ? (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16)>) \
+                       : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, false> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, false> : k_mix_tile_lds<E, R, V, 64, false>); \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)
@@ -2688,6 +3034,185 @@ int niidmix_update_rows_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y
     if (vec4) hipLaunchKernelGGL(k_update_rows<4>, grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, avg, n_chunks);
     else hipLaunchKernelGGL(k_update_rows<1>, grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, avg, n_chunks);
     return check_launch("k_update_rows");
+}
+
+int niidmix_sharded_create(int n_shards, const int *devices, niidmix_sharded **out) {
+    if (!out) return set_error(NIIDMIX_EINVAL, "null handle pointer");
+    *out = nullptr;
+    if (n_shards < 1 || !devices) return set_error(NIIDMIX_EINVAL, "n_shards < 1 or null device list");
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess) return set_error(NIIDMIX_EHIP, "hipGetDeviceCount failed");
+    for (int i = 0; i < n_shards; ++i)
+        if (devices[i] < 0 || devices[i] >= n_dev)
+            return set_error(NIIDMIX_EINVAL, "device %d of shard %d not visible (%d devices)", devices[i], i, n_dev);
+    niidmix_sharded *h = new niidmix_sharded;
+    h->n = n_shards;
+    h->dev.assign(devices, devices + n_shards);
+    for (int i = 0; i < n_shards && !h->loopback; ++i)
+        for (int j = 0; j < i; ++j)
+            if (devices[i] == devices[j]) h->loopback = true;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    int rc = NIIDMIX_OK;
+    h->ev_pack.assign(n_shards, nullptr);
+    h->ev_copy.assign(n_shards, nullptr);
+    for (int i = 0; i < n_shards && rc == NIIDMIX_OK; ++i) {
+        (void)hipSetDevice(devices[i]);
+        if (hipEventCreateWithFlags(&h->ev_pack[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_copy[i], hipEventDisableTiming) != hipSuccess)
+            rc = set_error(NIIDMIX_EHIP, "hipEventCreate failed");
+    }
+    (void)hipSetDevice(cur);
+    if (rc == NIIDMIX_OK && !h->loopback) {
+        const RcclApi *api = rccl_api();
+        if (!api) {
+            rc = set_error(NIIDMIX_EHIP, "librccl.so.1 could not be loaded");
+        } else {
+            h->comm.assign(n_shards, nullptr);
+            const ncclResult_t r = api->init_all(h->comm.data(), n_shards, devices);
+            if (r != ncclSuccess) {
+                h->comm.clear();
+                rc = set_error(NIIDMIX_EHIP, "ncclCommInitAll: %s", api->error(r));
+            }
+        }
+    }
+    if (rc != NIIDMIX_OK) {
+        niidmix_sharded_destroy(h);
+        return rc;
+    }
+    *out = h;
+    g_last_error[0] = '\0';
+    return NIIDMIX_OK;
+}
+
+int niidmix_sharded_destroy(niidmix_sharded *h) {
+    if (!h) return NIIDMIX_OK;
+    if (!h->comm.empty()) {
+        if (const RcclApi *api = rccl_api())
+            for (ncclComm_t c : h->comm)
+                if (c) (void)api->destroy(c);
+    }
+    for (hipEvent_t e : h->ev_pack) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h->ev_copy) if (e) (void)hipEventDestroy(e);
+    delete h;
+    return NIIDMIX_OK;
+}
+
+int niidmix_sharded_is_loopback(const niidmix_sharded *h) { return h && h->loopback ? 1 : 0; }
+
+int niidmix_mix_sharded_f32(niidmix_sharded *h, const niidmix_shard *sh, int64_t p, int mode) {
+    if (!h || !sh) return set_error(NIIDMIX_EINVAL, "null handle or shards");
+    if (p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    const int n = h->n;
+    for (int s = 0; s < n; ++s) {                 // host-side validation of every shard first
+        const niidmix_shard &a = sh[s];
+        if (a.device != h->dev[s]) return set_error(NIIDMIX_EINVAL, "shard %d: device %d, handle has %d", s, a.device, h->dev[s]);
+        if (a.n_local < 0 || a.rows_in < a.n_local || a.n_peers < 0 || a.n_peers > n - 1)
+            return set_error(NIIDMIX_EINVAL, "shard %d: bad sizes", s);
+        if (a.n_local > 0 && (!a.x || !a.y || !a.row_ptr || !a.col || !a.val))
+            return set_error(NIIDMIX_EINVAL, "shard %d: null slab or CSR", s);
+        if (a.n_peers > 0 && (!a.peer || !a.send_ptr || !a.recv_row || !a.recv_count))
+            return set_error(NIIDMIX_EINVAL, "shard %d: null exchange lists", s);
+        if (a.x && a.y && overlaps(a.x, a.rows_in * p, a.y, a.n_local * p))
+            return set_error(NIIDMIX_EALIAS, "shard %d: x and y overlap", s);
+        for (int j = 0; j < a.n_peers; ++j) {
+            const int q = a.peer[j];
+            if (q < 0 || q >= n || q == s) return set_error(NIIDMIX_EINVAL, "shard %d: bad peer %d", s, q);
+            if (a.send_ptr[j + 1] < a.send_ptr[j] || a.recv_count[j] < 0 || a.recv_row[j] < a.n_local ||
+                a.recv_row[j] + a.recv_count[j] > a.rows_in)
+                return set_error(NIIDMIX_EINVAL, "shard %d: bad exchange ranges for peer %d", s, q);
+            if (a.send_ptr[j + 1] > a.send_ptr[0] && (!a.send_rows || !a.send_buf))
+                return set_error(NIIDMIX_EINVAL, "shard %d: null send rows / buffer", s);
+            // the peer sends exactly what this shard receives from it
+            const niidmix_shard &b = sh[q];
+            int64_t cnt = -1;
+            for (int k = 0; k < b.n_peers; ++k)
+                if (b.peer[k] == s) cnt = b.send_ptr[k + 1] - b.send_ptr[k];
+            if (cnt != a.recv_count[j] && !(cnt < 0 && a.recv_count[j] == 0))
+                return set_error(NIIDMIX_EINVAL, "shard %d receives %lld rows from %d, which sends %lld",
+                                 s, (long long)a.recv_count[j], q, (long long)cnt);
+        }
+    }
+    if (p == 0) return NIIDMIX_OK;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    int rc = NIIDMIX_OK;
+    // 1. pack the rows every peer reads (each shard's stream)
+    for (int s = 0; s < n && rc == NIIDMIX_OK; ++s) {
+        const niidmix_shard &a = sh[s];
+        (void)hipSetDevice(a.device);
+        hipStream_t st = reinterpret_cast<hipStream_t>(a.stream);
+        const int64_t rows = a.n_peers ? a.send_ptr[a.n_peers] - a.send_ptr[0] : 0;
+        if (rows > 0) {
+            const bool v4 = p % 4 == 0 && aligned16(a.x) && aligned16(a.send_buf);
+            const int64_t cols = v4 ? 1024 : 256, nch = (p + cols - 1) / cols;
+            const int64_t items = rows * nch;
+            const dim3 grid((unsigned)(items < kMaxGrid ? items : kMaxGrid)), block(256);
+            const int32_t *r0 = a.send_rows + a.send_ptr[0];
+            float *b0 = a.send_buf;
+            if (v4) hipLaunchKernelGGL(k_gather_rows<4>, grid, block, 0, st, a.x, p, r0, rows, p, b0, p, nch);
+            else hipLaunchKernelGGL(k_gather_rows<1>, grid, block, 0, st, a.x, p, r0, rows, p, b0, p, nch);
+            rc = check_launch("k_gather_rows");
+        }
+        if (rc == NIIDMIX_OK && h->loopback && hipEventRecord(h->ev_pack[s], st) != hipSuccess)
+            rc = set_error(NIIDMIX_EHIP, "hipEventRecord failed");
+    }
+    // 2. exchange: RCCL point-to-point (one group over every shard), or device-to-device copies
+    //    when shards share a device
+    if (rc == NIIDMIX_OK && !h->loopback && n > 1) {
+        const RcclApi *api = rccl_api();
+        ncclResult_t r = api->group_start();
+        for (int s = 0; s < n && r == ncclSuccess; ++s) {
+            const niidmix_shard &a = sh[s];
+            hipStream_t st = reinterpret_cast<hipStream_t>(a.stream);
+            for (int j = 0; j < a.n_peers && r == ncclSuccess; ++j) {
+                const int64_t ns = a.send_ptr[j + 1] - a.send_ptr[j];
+                if (ns > 0) r = api->send(a.send_buf + (a.send_ptr[j] - a.send_ptr[0]) * p, (size_t)(ns * p),
+                                          ncclFloat32, a.peer[j], h->comm[s], st);
+                if (r == ncclSuccess && a.recv_count[j] > 0)
+                    r = api->recv(a.x + a.recv_row[j] * p, (size_t)(a.recv_count[j] * p), ncclFloat32,
+                                  a.peer[j], h->comm[s], st);
+            }
+        }
+        const ncclResult_t r2 = api->group_end();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            rc = set_error(NIIDMIX_EHIP, "RCCL halo exchange: %s", api->error(r != ncclSuccess ? r : r2));
+    } else if (rc == NIIDMIX_OK && h->loopback) {
+        for (int s = 0; s < n && rc == NIIDMIX_OK; ++s) {
+            const niidmix_shard &a = sh[s];
+            (void)hipSetDevice(a.device);
+            hipStream_t st = reinterpret_cast<hipStream_t>(a.stream);
+            for (int j = 0; j < a.n_peers && rc == NIIDMIX_OK; ++j) {
+                if (a.recv_count[j] == 0) continue;
+                const niidmix_shard &b = sh[a.peer[j]];
+                int k = 0;
+                while (b.peer[k] != s) ++k;                   // validated above
+                if (hipStreamWaitEvent(st, h->ev_pack[a.peer[j]], 0) != hipSuccess ||
+                    hipMemcpyAsync(a.x + a.recv_row[j] * p, b.send_buf + (b.send_ptr[k] - b.send_ptr[0]) * p,
+                                   (size_t)(a.recv_count[j] * p) * sizeof(float), hipMemcpyDeviceToDevice,
+                                   st) != hipSuccess)
+                    rc = set_error(NIIDMIX_EHIP, "loopback halo copy failed");
+            }
+            if (rc == NIIDMIX_OK && hipEventRecord(h->ev_copy[s], st) != hipSuccess)
+                rc = set_error(NIIDMIX_EHIP, "hipEventRecord failed");
+        }
+        // no shard packs again (next round) before every copy out of its buffer is done
+        for (int s = 0; s < n && rc == NIIDMIX_OK; ++s) {
+            (void)hipSetDevice(sh[s].device);
+            for (int q = 0; q < n; ++q)
+                if (q != s && hipStreamWaitEvent(reinterpret_cast<hipStream_t>(sh[s].stream), h->ev_copy[q], 0) != hipSuccess)
+                    rc = set_error(NIIDMIX_EHIP, "hipStreamWaitEvent failed");
+        }
+    }
+    // 3. mix every shard's rows over [local | halo] (stream-ordered after its receives)
+    for (int s = 0; s < n && rc == NIIDMIX_OK; ++s) {
+        const niidmix_shard &a = sh[s];
+        if (a.n_local == 0) continue;
+        (void)hipSetDevice(a.device);
+        rc = niidmix_mix_csr_f32(a.x, p, a.y, p, a.n_local, p, a.row_ptr, a.col, a.val, mode, a.stream);
+    }
+    (void)hipSetDevice(cur);
+    return rc;
 }
 
 int niidmix_copy2d_async(void *dst, int64_t dpitch_bytes, const void *src, int64_t spitch_bytes,

@@ -41,7 +41,16 @@ class TileLdsPlanC(ctypes.Structure):
     _fields_ = [("n_sub", _i64), ("rt", _i32), ("n_grp", _i32), ("max_src", _i32), ("max_tiles", _i32),
                 ("sub_ptr", _vp), ("sub_rows", _vp), ("sub_slot", _vp), ("sub_wself", _vp),
                 ("pos_slot", _vp), ("pos_mask", _vp), ("pos_w", _vp), ("grp_tile_ptr", _vp),
-                ("grp_src_ptr", _vp), ("grp_src_rows", _vp)]
+                ("grp_src_ptr", _vp), ("grp_src_rows", _vp), ("seg_ptr", _vp), ("seg", _vp),
+                ("seg_w", _vp)]
+
+
+class ShardC(ctypes.Structure):
+    """Mirror of struct niidmix_shard (include/niidmix.h)."""
+    _fields_ = [("device", _i32), ("n_peers", _i32), ("n_local", _i64), ("rows_in", _i64),
+                ("x", _vp), ("y", _vp), ("row_ptr", _vp), ("col", _vp), ("val", _vp),
+                ("peer", _vp), ("send_ptr", _vp), ("send_rows", _vp), ("send_buf", _vp),
+                ("recv_row", _vp), ("recv_count", _vp), ("stream", _vp)]
 
 
 # every symbol include/niidmix.h declares, with its ctypes signature
@@ -50,6 +59,8 @@ SIGNATURES = {
     "niidmix_last_error": (ctypes.c_char_p, []),
     "niidmix_mix_csr_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
                                            ctypes.c_int, _vp]),
+    "niidmix_mix_ell_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp, _vp,
+                                           _vp, ctypes.c_int, _vp]),
     "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,
@@ -68,6 +79,10 @@ SIGNATURES = {
     "niidmix_update_rows_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "niidmix_sgd_step_rows_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _vp, _i64,
                                                  ctypes.c_float, _vp]),
+    "niidmix_sharded_create": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
+    "niidmix_sharded_destroy": (ctypes.c_int, [_vp]),
+    "niidmix_sharded_is_loopback": (ctypes.c_int, [_vp]),
+    "niidmix_mix_sharded_f32": (ctypes.c_int, [_vp, ctypes.POINTER(ShardC), _i64, ctypes.c_int]),
     "niidmix_hbm_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, _vp]),
     "niidmix_hbm_free": (None, [_vp, ctypes.c_ssize_t, ctypes.c_int, _vp]),
     "niidmix_copy2d_async": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp]),

@@ -2,6 +2,7 @@
 
 Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
+  mix_ell(x, ell_col, ell_val, ell_len, out, k, mode)  k_mix_ell  the same, low-degree graphs
   mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, res_member,
              row_ptr, col, val, out, max_clique, max_clique_res)
                                                     k_mix_clique (fast, HBM-bound; the CSR is the
@@ -20,13 +21,14 @@ implementation and no fallback.
 """
 import ctypes
 import os
+from typing import Optional
 
 import numpy as np
 import torch
 
 from . import _lib
 from .factor import build_clique_plan
-from .tile import LDS_MAX_WAVES, build_tile_lds_plan, build_tile_plan
+from .tile import LDS_MAX_WAVES, build_tile_lds_plan, build_tile_plan, build_tile_segments
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -111,6 +113,42 @@ def mix_csr(x: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor, val: torc
                                       row_ptr.data_ptr(), col.data_ptr(), val.data_ptr(), int(mode),
                                       _stream(x))
     _lib.check(rc, "niidmix::mix_csr")
+
+
+@torch.library.custom_op("niidmix::mix_ell", mutates_args=("out",))
+def mix_ell(x: torch.Tensor, ell_col: torch.Tensor, ell_val: torch.Tensor, ell_len: torch.Tensor,
+            out: torch.Tensor, k: int, mode: int) -> None:
+    """mix_csr over the ELL layout of the same rows (low-degree graphs; include/niidmix.h)."""
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    _req(out.device == x.device, "x and out must be on the same device")
+    n = out.shape[0]
+    _vec("ell_col", ell_col, torch.int32, x.device, n * k)
+    _vec("ell_val", ell_val, torch.float32, x.device, n * k)
+    _vec("ell_len", ell_len, torch.int32, x.device, n)
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_ell_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n, x.shape[1],
+                                      int(k), ell_col.data_ptr(), ell_val.data_ptr(),
+                                      ell_len.data_ptr(), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_ell")
+
+
+def ell_layout(csr):
+    """(k, col [N*k], val [N*k], len [N]) of the CSR's rows, padded to k in {3, 5, 8} entries, or
+    None when a row has more than 8 entries.  Padding repeats the row's self entry (never summed:
+    the kernel stops at len)."""
+    lens = np.diff(csr.row_ptr)
+    if csr.n == 0 or lens.max() > 8:
+        return None
+    k = 3 if lens.max() <= 3 else 5 if lens.max() <= 5 else 8
+    n = csr.n
+    col = np.repeat(np.arange(n, dtype=np.int32), k).reshape(n, k)
+    val = np.zeros((n, k), np.float32)
+    j = np.arange(int(csr.row_ptr[-1])) - np.repeat(csr.row_ptr[:-1], lens)
+    r = np.repeat(np.arange(n), lens)
+    col[r, j] = csr.col
+    val[r, j] = csr.val
+    return k, col.reshape(-1), val.reshape(-1), lens.astype(np.int32)
 
 
 @torch.library.custom_op("niidmix::mix_clique", mutates_args=("out",))
@@ -212,7 +250,10 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                  sub_slot: torch.Tensor, sub_wself: torch.Tensor, pos_slot: torch.Tensor,
                  pos_mask: torch.Tensor, pos_w: torch.Tensor, grp_tile_ptr: torch.Tensor,
                  grp_src_ptr: torch.Tensor, grp_src_rows: torch.Tensor, out: torch.Tensor, rt: int,
-                 max_src: int, max_tiles: int, mode: int) -> None:
+                 max_src: int, max_tiles: int, mode: int, seg_ptr: Optional[torch.Tensor] = None,
+                 seg: Optional[torch.Tensor] = None, seg_w: Optional[torch.Tensor] = None) -> None:
+    """seg_ptr / seg / seg_w: the plan's segments (niidmix.tile.build_tile_segments, RT 16 only):
+    the kernel's segment loop instead of the per-position loop; bit-identical results."""
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -228,13 +269,22 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
     _vec("grp_tile_ptr", grp_tile_ptr, torch.int32, dev)
     _vec("grp_src_ptr", grp_src_ptr, torch.int32, dev, g + 1)
     _vec("grp_src_rows", grp_src_rows, torch.int32, dev)
+    segs = (None, None, None)
+    if seg_ptr is not None:
+        _req(rt == 16 and seg is not None and seg_w is not None,
+             "segments: RT 16 plans, with seg_ptr, seg and seg_w")
+        _vec("seg_ptr", seg_ptr, torch.int32, dev, t + 1)
+        _vec("seg", seg, torch.int32, dev)
+        _req(seg.numel() % 4 == 0 and seg.data_ptr() % 16 == 0, "seg: [S, 4] int32, 16-B aligned")
+        _vec("seg_w", seg_w, torch.float32, dev, 2 * t)
+        segs = (seg_ptr.data_ptr(), seg.data_ptr(), seg_w.data_ptr())
     _no_overlap(x, out)
     some = sub_ptr.data_ptr()
     plan = _lib.TileLdsPlanC(t, int(rt), g, int(max_src), int(max_tiles), sub_ptr.data_ptr(),
                              sub_rows.data_ptr(), sub_slot.data_ptr(), sub_wself.data_ptr(),
                              pos_slot.data_ptr() or some, pos_mask.data_ptr() or some,
                              pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
-                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr())
+                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs)
     rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
                                            out.shape[0], x.shape[1], ctypes.byref(plan), int(mode),
                                            _stream(x))
@@ -350,7 +400,9 @@ _LAZY = {
     "tlds": "tlds", "tlds_reason": "tlds", "l_sub_ptr": "tlds", "l_sub_rows": "tlds",
     "l_sub_slot": "tlds", "l_sub_wself": "tlds", "l_pos_slot": "tlds", "l_pos_mask": "tlds",
     "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
+    "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
     "w_dense": "dense",
+    "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell",
 }
 
 
@@ -399,6 +451,7 @@ class Mixer:
         self.dense = (csr.n_in == csr.n and csr.nnz >= dense_threshold * self.n * self.n
                       and self.n >= 64)
         self._host = {}           # host-side plans, shared with the Mixers .to() makes
+        self.use_segments = True  # RT-16 LDS tiles: segment loop where segments built
 
     def to(self, device):
         """The same operator on another device, sharing the host-side plans (built once)."""
@@ -495,6 +548,24 @@ class Mixer:
         self.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
         self.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
         self.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
+        # segment loop (RT 16): runs of consecutive LDS slots read at immediate offsets
+        # (niidmix.tile.build_tile_segments); NIIDMIX_TLDS_SEG=0 keeps the per-position loop
+        self.tseg = None
+        if tp.rt == 16 and os.environ.get("NIIDMIX_TLDS_SEG", "1") != "0":
+            self.tseg = self._hosted(("tseg", tp.rt), lambda: build_tile_segments(lp))
+        if self.tseg is not None:
+            self.s_seg_ptr = torch.from_numpy(self.tseg.seg_ptr).to(dev)
+            self.s_seg = torch.from_numpy(np.ascontiguousarray(self.tseg.seg)).to(dev)
+            self.s_seg_w = torch.from_numpy(self.tseg.seg_w).to(dev)
+
+    def _build_ell(self):
+        lay = self._hosted("ell", lambda: ell_layout(self.csr))
+        self.ell = None if lay is None else lay[0]
+        if lay is not None:
+            k, col, val, ln = lay
+            self.e_col = torch.from_numpy(col).to(self.device)
+            self.e_val = torch.from_numpy(val).to(self.device)
+            self.e_len = torch.from_numpy(ln).to(self.device)
 
     def _build_dense(self):
         self.w_dense = torch.from_numpy(self.csr.dense()).to(self.device)
@@ -563,7 +634,9 @@ class Mixer:
             # degree >= 8 (ring / grid rows read 2-4 sources: CSR gather)
             if self.tlds is not None and (x is None or _lds_ok(x)) and (out is None or _lds_ok(out)):
                 return "tile-lds-exact"
-            return "tile-exact" if self.tile is not None else "csr-exact"
+            if self.tile is not None:
+                return "tile-exact"
+            return "ell-exact" if self.ell is not None else "csr-exact"
         if self.factored_safe and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:
@@ -571,7 +644,7 @@ class Mixer:
         if self.plan is not None and self.tlds is not None and (x is None or _lds_ok(x)) and \
                 (out is None or _lds_ok(out)):
             return "tile-lds-fast"               # clique graph with removed edges
-        return "csr-fast"
+        return "ell-fast" if self.ell is not None else "csr-fast"
 
     def __call__(self, x, out=None, mode="fast", kernel=None):
         if out is None:
@@ -582,6 +655,10 @@ class Mixer:
             mix_csr(x, self.row_ptr, self.col, self.val, out, EXACT | hint)
         elif k == "csr-fast":
             mix_csr(x, self.row_ptr, self.col, self.val, out, FAST | hint)
+        elif k in ("ell-exact", "ell-fast"):
+            _req(self.ell is not None, "no ELL layout: a row has more than 8 entries")
+            mix_ell(x, self.e_col, self.e_val, self.e_len, out, self.ell,
+                    EXACT if k == "ell-exact" else FAST)
         elif k in ("tile-exact", "tile-fast"):
             _req(self.tile is not None, f"no tile plan: {self.tile_reason}")
             mix_tile(x, self.t_sub_ptr, self.t_sub_rows, self.t_sub_wself, self.t_pos_src,
@@ -590,10 +667,13 @@ class Mixer:
         elif k in ("tile-lds-exact", "tile-lds-fast"):
             _req(self.tlds is not None, f"no LDS tile plan: {self.tlds_reason}")
             lp = self.tlds
+            ts = self.tseg
+            segs = (self.s_seg_ptr, self.s_seg, self.s_seg_w) if \
+                self.use_segments and ts is not None and ts.lp is lp else ()
             mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
                          self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
                          self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,
-                         lp.max_tiles, EXACT if k == "tile-lds-exact" else FAST)
+                         lp.max_tiles, EXACT if k == "tile-lds-exact" else FAST, *segs)
         elif k == "clique":
             _req(self.plan is not None, f"no clique plan: {self.plan_reason}")
             mix_clique(x, *self._clique_args(), out, self.plan.max_clique,

@@ -438,3 +438,115 @@ class StripedMixer:
         if events is not None:
             events[1].record(cur)
         return out
+
+
+class LocalShardedRound:
+    """Node shards over several GPUs of THIS process (the simulator's own model, run.py:136)
+    through the C-ABI sharded round (niidmix_mix_sharded_f32, include/niidmix.h): per round and
+    shard, pack the rows peers read -> RCCL point-to-point halo exchange (one group over every
+    shard; device-to-device copies when shards share a device) -> niidmix_mix_csr_f32 over
+    [local rows | halo rows].  The ShardPlan and the RCCL communicators are built once per
+    topology.  Exact mode is bitwise the single-GPU round (every row keeps its operand order).
+
+    Slabs are ping-pong pairs per shard: round k reads xs[k % 2] and writes the local rows of
+    xs[(k + 1) % 2]; scatter() fills the current input, gather() returns the current state."""
+
+    def __init__(self, csr, cliques, devices, p):
+        import ctypes
+        from . import _lib
+        self._lib = _lib
+        self.devices = [torch.device(d) for d in devices]
+        self.world = len(self.devices)
+        self.p = p
+        self.plan = ShardPlan(csr, cliques, self.world)
+        self.shards = [self.plan.local(r) for r in range(self.world)]
+        self.n_total = csr.n
+        self._keep = []
+        self.xs, self.bufs, self.streams, self.host = [], [], [], []
+        self.cur = 0
+        for r, (sh, dev) in enumerate(zip(self.shards, self.devices)):
+            rows_in, nl = sh.rows_in, sh.n_local
+            xs = [torch.zeros((max(rows_in, 1), p), dtype=torch.float32, device=dev) for _ in range(2)]
+            peers = sorted(set(sh.send) | set(sh.recv))
+            send = [np.asarray(sh.send.get(q, np.zeros(0, np.int64)), np.int64) for q in peers]
+            send_ptr = np.concatenate([[0], np.cumsum([len(v) for v in send])]).astype(np.int64)
+            send_rows = torch.from_numpy(np.concatenate(send).astype(np.int32) if send else
+                                         np.zeros(0, np.int32)).to(dev)
+            send_buf = torch.empty((max(int(send_ptr[-1]), 1), p), dtype=torch.float32, device=dev)
+            recv_row = np.asarray([sh.recv[q][0] if q in sh.recv else nl for q in peers], np.int64)
+            recv_cnt = np.asarray([sh.recv[q][1] + sh.recv[q][2] if q in sh.recv else 0
+                                   for q in peers], np.int64)
+            peer_arr = np.asarray(peers, np.int32)
+            rp = torch.from_numpy(sh.csr.row_ptr).to(dev)
+            cl = torch.from_numpy(sh.csr.col).to(dev)
+            vl = torch.from_numpy(sh.csr.val).to(dev)
+            self.xs.append(xs)
+            self.bufs.append(send_buf)
+            self.streams.append(torch.cuda.Stream(dev))
+            host = dict(peer=peer_arr, send_ptr=send_ptr, recv_row=recv_row, recv_cnt=recv_cnt)
+            self.host.append(host)
+            self._keep += [rp, cl, vl, send_rows, peer_arr, send_ptr, recv_row, recv_cnt]
+            host.update(rp=rp, cl=cl, vl=vl, send_rows=send_rows)
+        dev_ids = (ctypes.c_int * self.world)(*[d.index if d.index is not None else 0
+                                                for d in self.devices])
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.niidmix_sharded_create(self.world, dev_ids, ctypes.byref(h)),
+                   "niidmix_sharded_create")
+        self.handle = h
+        self.loopback = bool(_lib.lib.niidmix_sharded_is_loopback(h))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            self._lib.lib.niidmix_sharded_destroy(h)
+            self.handle = None
+
+    def _shard_structs(self):
+        import ctypes
+        from ._lib import ShardC
+        arr = (ShardC * self.world)()
+        a, b = self.cur, 1 - self.cur
+        for r, (sh, hd) in enumerate(zip(self.shards, self.host)):
+            c = arr[r]
+            c.device = self.devices[r].index if self.devices[r].index is not None else 0
+            c.n_peers = len(hd["peer"])
+            c.n_local, c.rows_in = sh.n_local, sh.rows_in
+            c.x, c.y = self.xs[r][a].data_ptr(), self.xs[r][b].data_ptr()
+            c.row_ptr, c.col, c.val = hd["rp"].data_ptr(), hd["cl"].data_ptr(), hd["vl"].data_ptr()
+            ptr = lambda v: v.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+            c.peer, c.send_ptr = ptr(hd["peer"]), ptr(hd["send_ptr"])
+            c.send_rows = hd["send_rows"].data_ptr() if hd["send_rows"].numel() else None
+            c.send_buf = self.bufs[r].data_ptr()
+            c.recv_row, c.recv_count = ptr(hd["recv_row"]), ptr(hd["recv_cnt"])
+            c.stream = self.streams[r].cuda_stream
+        return arr
+
+    def scatter(self, x):
+        """x: the global [N, p] slab (rank order, any device) -> every shard's local input rows."""
+        for r, sh in enumerate(self.shards):
+            idx = torch.from_numpy(np.asarray(sh.nodes, np.int64)).to(x.device)
+            self.xs[r][self.cur][:sh.n_local].copy_(x.index_select(0, idx))
+        torch.cuda.synchronize()
+
+    def gather(self):
+        """The current global state [N, p] on the CPU, rank order."""
+        torch.cuda.synchronize()
+        out = torch.empty((self.n_total, self.p), dtype=torch.float32)
+        for r, sh in enumerate(self.shards):
+            out[torch.from_numpy(np.asarray(sh.nodes, np.int64))] = \
+                self.xs[r][self.cur][:sh.n_local].cpu()
+        return out
+
+    def __call__(self, mode="exact"):
+        """One round on every shard (enqueued on the shards' streams, after each device's current
+        stream), then the roles of the two slabs swap."""
+        from .ops import EXACT, FAST
+        for r in range(self.world):
+            self.streams[r].wait_stream(torch.cuda.current_stream(self.devices[r]))
+        arr = self._shard_structs()
+        rc = self._lib.lib.niidmix_mix_sharded_f32(self.handle, arr, self.p,
+                                                   EXACT if mode == "exact" else FAST)
+        self._lib.check(rc, "niidmix_mix_sharded_f32")
+        for r in range(self.world):
+            torch.cuda.current_stream(self.devices[r]).wait_stream(self.streams[r])
+        self.cur = 1 - self.cur

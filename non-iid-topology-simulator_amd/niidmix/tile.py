@@ -344,3 +344,166 @@ def apply_np(plan, x, exact=True, average_only=False):
                 acc = (np.float64(w) * x[src].astype(np.float64) + acc).astype(np.float32)
         y[row] = acc if average_only else z + acc
     return y
+
+
+SEG_HARD = 1 << 30           # seg word 0 flag: a MASKED position (rows in word 1, weight in word 2)
+SEG_WORDS = 4
+SEG_SLOT = 0xfff             # slot field of word 0
+
+
+@dataclass
+class TileSegments:
+    """The positions of an RT-16 LDS tile plan cut into SEGMENTS for k_mix_tile_lds's segment loop
+    (include/niidmix.h, niidmix_tile_lds_plan.seg*).  A fast segment is a run of positions that
+      * read CONSECUTIVE LDS slots s0, s0+1, ... (slots are numbered in list order, so a tile's
+        positions mostly do): the kernel reads position i at one base address + i * row bytes, an
+        immediate offset, with no per-position descriptor;
+      * carry a uniform weight, one of the tile's two (w0, w1 in seg_w; bit i of wsel picks w1);
+      * are taken by every tile row, or by all rows but one (bit i of skip), where the k-th such
+        position of the segment skips tile row r0 + k (a tile's rows follow the list order, so
+        their own positions come in that order).
+    Any other position becomes MASKED entries (word 0 = slot | SEG_HARD, word 1 = the rows taking it,
+    word 2 = the weight's fp32 bits), one per weight class of its rows: each row still takes the
+    position once, at this point of its own order, so exact results are unchanged.
+    seg [S, 4] int32: runs s0 | L << 12 | r0 << 20, wsel bits, skip bits, 0 (slots < 4096,
+    L <= 32); None when a group stages 4096 rows or more (never: LDS holds ~400).
+    seg_ptr [T+1] int32 (segments of tile t), seg_w [T, 2] fp32."""
+    seg_ptr: np.ndarray
+    seg: np.ndarray
+    seg_w: np.ndarray
+    lp: object = None            # the TileLdsPlan these segments cut
+
+    @property
+    def n_seg(self):
+        return len(self.seg)
+
+
+def build_tile_segments(lp, max_len=32):
+    """TileSegments of a TileLdsPlan (RT 16 tiles; any RT works, the kernel uses them at RT 16)."""
+    tp = lp.tile
+    rt = tp.rt
+    full = (1 << rt) - 1
+    if lp.max_src + 2 > SEG_SLOT:
+        return None
+    slots = (lp.pos_slot & (POS_UNIFORM - 1)).astype(np.int64)
+    uni = (lp.pos_slot & POS_UNIFORM) != 0
+    mask = tp.pos_mask.astype(np.int64)
+    w0s = tp.pos_w.reshape(-1, rt)[:, 0] if tp.n_pos else np.zeros(0, np.float32)
+    seg_ptr, segs, seg_w = [0], [], []
+    for t in range(tp.n_sub):
+        b, e = int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])
+        real = 0
+        for r in range(rt):
+            if tp.sub_rows[t * rt + r] >= 0:
+                real |= 1 << r
+        ws = []
+        for k in range(b, e):                       # the tile's first two uniform weights
+            if uni[k] and w0s[k] not in ws:
+                ws.append(w0s[k])
+                if len(ws) == 2:
+                    break
+        while len(ws) < 2:
+            ws.append(np.float32(0.0))
+        wbits = [np.float32(v).view(np.uint32) for v in ws]
+        cur = None
+        for k in range(b, e):
+            miss = int(~mask[k] & full)
+            wk = np.float32(w0s[k]).view(np.uint32)
+            easy = bool(uni[k]) and (miss & (miss - 1)) == 0 and wk in wbits
+            if not easy:
+                if cur is not None:
+                    segs.append(cur)
+                    cur = None
+                # MASKED entries: the rows that take the position, one entry per weight class
+                # (each row still takes the position once, at this point of its own order)
+                m = int(tp.pos_mask[k]) & real
+                wr = tp.pos_w[k * rt:(k + 1) * rt]
+                classes = {}
+                for r in range(rt):
+                    if (m >> r) & 1:
+                        classes.setdefault(int(np.float32(wr[r]).view(np.uint32)), 0)
+                        classes[int(np.float32(wr[r]).view(np.uint32))] |= 1 << r
+                for wb, cm in classes.items():
+                    segs.append(["M", int(slots[k]), cm, wb])
+                continue
+            skip = miss.bit_length() - 1 if miss else -1
+            sel = 1 if (wk == wbits[1] and wk != wbits[0]) else 0
+            ok = (cur is not None and slots[k] == cur[0] + cur[1] and cur[1] < max_len and
+                  (skip < 0 or cur[8] is None or cur[8] == skip))
+            if not ok:
+                if cur is not None:
+                    segs.append(cur)
+                cur = [int(slots[k]), 0, 0, 0, 0, 0, 0, k, None]
+            i = cur[1]
+            if sel:
+                if i < 32:
+                    cur[2] |= 1 << i
+                else:
+                    cur[3] |= 1 << (i - 32)
+            if skip >= 0:
+                if cur[8] is None:
+                    cur[6] = skip                       # r0: the first skipped row
+                if i < 32:
+                    cur[4] |= 1 << i
+                else:
+                    cur[5] |= 1 << (i - 32)
+                cur[8] = skip + 1
+            cur[1] += 1
+        if cur is not None:
+            segs.append(cur)
+        seg_ptr.append(len(segs))
+        seg_w.append(ws)
+    arr = np.zeros((len(segs), SEG_WORDS), np.int64)
+    for i, sg in enumerate(segs):
+        if sg[0] == "M":
+            _, slot, cm, wb = sg
+            arr[i] = [slot | SEG_HARD, cm, wb, 0]
+        else:
+            s0, ln, wlo, _, klo, _, r0 = sg[:7]
+            arr[i] = [s0 | (ln << 12) | (r0 << 20), wlo, klo, 0]
+    arr = (arr & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    return TileSegments(seg_ptr=np.asarray(seg_ptr, np.int32), seg=arr.reshape(-1, SEG_WORDS),
+                        seg_w=np.asarray(seg_w, np.float32).reshape(-1, 2), lp=lp)
+
+
+def segments_row_lists(lp, ts):
+    """{row: [(src, w), ...]} as the segment loop applies them (self first) -- for checks."""
+    tp = lp.tile
+    rt = tp.rt
+    src_rows = lp.grp_src_rows
+    gtp = lp.grp_tile_ptr
+    grp_of = np.zeros(tp.n_sub, np.int64)
+    for gi in range(len(gtp) - 1):
+        grp_of[gtp[gi]:gtp[gi + 1]] = gi
+    out = {}
+    seg = ts.seg.view(np.uint32).astype(np.int64)
+    for t in range(tp.n_sub):
+        base = int(lp.grp_src_ptr[grp_of[t]])
+        rows = tp.sub_rows[t * rt:(t + 1) * rt]
+        lists = {r: [(int(rows[r]), np.float32(tp.sub_wself[t * rt + r]))]
+                 for r in range(rt) if rows[r] >= 0}
+        w0, w1 = ts.seg_w[t]
+        for s in seg[ts.seg_ptr[t]:ts.seg_ptr[t + 1]]:
+            hd = int(s[0])
+            if hd & SEG_HARD:
+                src = int(src_rows[base + (hd & SEG_SLOT)])
+                m, w = int(s[1]), np.uint32(s[2]).view(np.float32)
+                for r in lists:
+                    if (m >> r) & 1:
+                        lists[r].append((src, np.float32(w)))
+                continue
+            s0, ln, r_skip = hd & SEG_SLOT, (hd >> 12) & 0xff, (hd >> 20) & 0xff
+            wsel, skip = int(s[1]), int(s[2])
+            for i in range(ln):
+                src = int(src_rows[base + s0 + i])
+                w = w1 if (wsel >> i) & 1 else w0
+                skipped = -1
+                if (skip >> i) & 1:
+                    skipped = r_skip
+                    r_skip += 1
+                for r in lists:
+                    if r != skipped:
+                        lists[r].append((src, np.float32(w)))
+        for r, lst in lists.items():
+            out[int(rows[r])] = lst
+    return out

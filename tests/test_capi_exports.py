@@ -112,3 +112,12 @@ def test_argument_errors_without_gpu():
     assert L.niidmix_stream_copy_f32(16, 32, 8, None) == _lib.EALIAS
     assert L.niidmix_stream_copy_f32(None, 32, 8, None) == _lib.EINVAL
     assert L.niidmix_stream_copy_f32(16, 1024, 0, None) == _lib.OK
+    h = ctypes.c_void_p()
+    assert L.niidmix_sharded_create(0, None, ctypes.byref(h)) == _lib.EINVAL and not h.value
+    assert L.niidmix_sharded_destroy(None) == _lib.OK
+    assert L.niidmix_mix_sharded_f32(None, None, 4, 0) == _lib.EINVAL
+    E = L.niidmix_mix_ell_f32
+    assert E(16, 4, 1024, 4, 1, 4, 9, 8, 8, 8, 0, None) == _lib.EUNSUPPORTED            # width 9
+    assert E(16, 4, 1024, 4, 1, 4, 4, 8, 8, 8, 0, None) == _lib.EINVAL                  # unpadded width
+    assert E(16, 4, 16, 4, 1, 4, 3, 8, 8, 8, 0, None) == _lib.EALIAS
+    assert E(None, 4, 1024, 4, 1, 4, 3, 8, 8, 8, 0, None) == _lib.EINVAL

@@ -95,15 +95,15 @@ def test_fc1000_blocked_bigclique_fullsize(gpu, oracle_mod):
 
 @pytest.mark.parametrize("mode", ["fast", "exact"])
 def test_ring100_p62006_hipgraph(mode, gpu, oracle_mod):
-    """bench.py --config ring100 (P = 62006, rows 8-byte aligned: the float2 CSR path, 2 chunks per
-    wave for a low-degree graph) with the rounds captured in ONE hipGraph, as the bench times it:
+    """bench.py --config ring100 (P = 62006, rows 8-byte aligned: the float2 path of the ELL kernel,
+    4 chunks per wave) with the rounds captured in ONE hipGraph, as the bench times it:
     two ping-pong rounds per replay, each checked against the oracle applied to that round's own
     GPU input (bitwise in exact mode)."""
     g, csr = _golden_csr("ring100_p257")
     m = _mixer(csr, None, gpu)
     p = 62006
     kernel = m.kernel_for(mode)
-    assert kernel == ("csr-fast" if mode == "fast" else "csr-exact")
+    assert kernel == ("ell-fast" if mode == "fast" else "ell-exact")
     a = torch.randn(100, p, device=gpu, generator=torch.Generator(device=gpu).manual_seed(2))
     b = torch.empty_like(a)
     m(a, out=b, kernel=kernel, mode=mode)                   # warm-up outside the capture
@@ -246,3 +246,25 @@ def test_fc_block32_layout_bitwise(gpu):
     y2 = memory.empty_blocked(n, p, gpu, 32)
     m.mix_blocked(memory.to_blocked(x, 32), y2, p)
     assert torch.equal(memory.from_blocked(y1, p), memory.from_blocked(y2, p))
+
+
+def test_fc1000_dense_mfma_fullsize_windows(gpu, oracle_mod):
+    """configs[3] through the MFMA GEMM (bench.py --config fc1000 --kernel dense) at the P = 2^20 it
+    is profiled at: column windows at the start, middle and end (the last 128-column tile) against
+    the oracle within the tolerance, and column sums preserved over every column."""
+    from niidmix import memory
+    from niidmix.topology import mh_csr
+    n = 1000
+    csr = mh_csr(n, {i: [j for j in range(n) if j != i] for i in range(n)})
+    m = _mixer(csr, None, gpu)
+    x = memory.empty_slab(n, P_FULL, gpu)
+    x.normal_(generator=torch.Generator(device=gpu).manual_seed(6))
+    y = memory.empty_slab(n, P_FULL, gpu)
+    m(x, out=y, kernel="dense")
+    torch.cuda.synchronize()
+    for c0 in (0, P_FULL // 2 - 64, P_FULL - 384):
+        xw = x[:, c0:c0 + 384].cpu().numpy()
+        _check_block(oracle_mod, csr, xw, y[:, c0:c0 + 384].cpu().numpy(), c0)
+    gap = torch.max(torch.abs(torch.sum(x, 0, dtype=torch.float64) -
+                              torch.sum(y, 0, dtype=torch.float64))).item()
+    assert gap < 1e-3

@@ -27,19 +27,21 @@ def _mixer(g, dev, **kw):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-exact", "tile-exact"])
+@pytest.mark.parametrize("kernel", ["csr-exact", "tile-exact", "ell-exact"])
 def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
     g = load_golden(name)
     m = _mixer(g, gpu)
     if kernel == "tile-exact" and m.tile is None:
         m = _tile_mixer(g, gpu, 8)
+    if kernel == "ell-exact" and m.ell is None:
+        pytest.skip("a row has more than 8 entries")
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel=kernel).cpu().numpy()
     assert oracle_mod.bitwise_equal(y, g["y"]), name
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "tile-fast"])
+@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "tile-fast", "ell-fast"])
 def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
     """Every fast kernel on every golden case, non-finite fixtures included: NaN where the
     reference has NaN, the same inf where it has inf (the factored and GEMM kernels recompute
@@ -52,6 +54,8 @@ def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
         pytest.skip(f"no clique plan ({m.plan_reason}) or p % 4")
     if kernel == "tile-fast" and m.tile is None:
         m = _tile_mixer(g, gpu, 16)
+    if kernel == "ell-fast" and m.ell is None:
+        pytest.skip("a row has more than 8 entries")
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel=kernel).cpu().numpy()
     bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
@@ -118,6 +122,11 @@ def _tile_lds_mixer(g, dev, rt):
     m.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
     m.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
     m.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
+    m.tseg = tile.build_tile_segments(lp) if rt == 16 else None
+    if m.tseg is not None:
+        m.s_seg_ptr = torch.from_numpy(m.tseg.seg_ptr).to(dev)
+        m.s_seg = torch.from_numpy(np.ascontiguousarray(m.tseg.seg)).to(dev)
+        m.s_seg_w = torch.from_numpy(m.tseg.seg_w).to(dev)
     return m
 
 
@@ -179,6 +188,55 @@ def test_tile_lds_narrow_items_bitwise(name, cols, gpu, oracle_mod, monkeypatch)
     assert oracle_mod.bitwise_equal(y, g["y"]), (name, cols)
 
 
+@pytest.mark.parametrize("name", golden_cases())
+def test_tile_lds_segment_loop_bitwise(name, gpu, oracle_mod):
+    """RT-16 LDS tiles with the segment loop (runs of consecutive slots at immediate offsets,
+    MASKED entries for the rest; niidmix.tile.build_tile_segments) and with the per-position loop:
+    both bit-identical to the reference, exact and average-only; fast within 1e-5."""
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    m = _tile_lds_mixer(g, gpu, 16)
+    assert m.tseg is not None and m.tseg.lp is m.tlds
+    x = torch.from_numpy(g["x"]).to(gpu)
+    for seg in (True, False):
+        m.use_segments = seg
+        y = m(x, kernel="tile-lds-exact").cpu().numpy()
+        assert oracle_mod.bitwise_equal(y, g["y"]), (name, seg)
+    ops = _ops()
+    lp = m.tlds
+    out = torch.empty_like(x)
+    ops.mix_tile_lds(x, m.l_sub_ptr, m.l_sub_rows, m.l_sub_slot, m.l_sub_wself, m.l_pos_slot,
+                     m.l_pos_mask, m.l_pos_w, m.l_grp_tile_ptr, m.l_grp_src_ptr, m.l_grp_src_rows,
+                     out, 16, lp.max_src, lp.max_tiles, ops.EXACT | ops.AVERAGE_ONLY, m.s_seg_ptr,
+                     m.s_seg, m.s_seg_w)
+    ref = oracle_mod.mix_exact_c(g["x"], g["row_ptr"], g["col"], g["val"], average_only=True)
+    assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref), name
+    if np.all(np.isfinite(g["x"])):
+        m.use_segments = True
+        yf = m(x, kernel="tile-lds-fast").cpu().numpy()
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        ok, worst = oracle_mod.check_tolerance(yf, g["y"], bound, rtol=RTOL)
+        assert ok, (name, worst)
+
+
+@pytest.mark.parametrize("n,size,inter", [(1000, 10, "fully-connected"), (600, 30, "smallworld"),
+                                          (2000, 100, "ring")])
+def test_tile_lds_segment_loop_masked_heavy(n, size, inter, gpu, oracle_mod):
+    """Topologies whose tiles are mostly MASKED entries (cliques of 10: most positions are one
+    gateway row's inter-clique edge) or many-tile cliques (100 members, 7 tiles): the segment
+    loop is bitwise the C oracle, with 120-column items and a ragged last item (p = 1002)."""
+    from niidmix.generate import dcliques_csr
+    csr, cl = dcliques_csr(n, size, inter, 1337)
+    g = {"row_ptr": csr.row_ptr, "col": csr.col, "val": csr.val, "cliques": cl}
+    m = _tile_lds_mixer(g, gpu, 16)
+    assert m.tseg is not None
+    x = np.random.default_rng(n).standard_normal((n, 1002)).astype(np.float32)
+    y = m(torch.from_numpy(x).to(gpu), kernel="tile-lds-exact").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(x, csr.row_ptr, csr.col, csr.val)
+    assert oracle_mod.bitwise_equal(y, ref), (n, size, inter)
+
+
 def test_tile_lds_narrow_items_float2(gpu, oracle_mod):
     """The 1000-node d-cliques plan picks 120-column items by itself (109 staged rows); p = 1002
     (p % 4 == 2: float2 staging) ends in a ragged item.  Bitwise against the C oracle."""
@@ -224,8 +282,8 @@ def test_auto_kernel_choice(gpu):
                                              for i in range(n)]))
     assert ops.Mixer(csr=csr, device=gpu).kernel_for("fast") == "dense"
     g = load_golden("ring100_p257")
-    assert _mixer(g, gpu).kernel_for("fast") == "csr-fast"
-    assert _mixer(g, gpu).kernel_for("exact") == "csr-exact"   # degree 2: no tile plan
+    assert _mixer(g, gpu).kernel_for("fast") == "ell-fast"
+    assert _mixer(g, gpu).kernel_for("exact") == "ell-exact"   # degree 2: no tile plan, ELL rows
 
 
 def _dcliques_full(gpu, p, seed=0):
@@ -506,3 +564,63 @@ def test_multi_clique_tile_auto(n, inter, gpu, oracle_mod, monkeypatch):
     ok, worst = oracle_mod.check_tolerance(memory.from_blocked(yb, p)[pt].cpu().numpy(), ref, bound,
                                            rtol=RTOL)
     assert ok, worst
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("name,p", [("ring100_p257", 62006), ("grid49_p20", 4099), ("n2_ring_linear7850", 7850),
+                                    ("nonfinite_ring8_p16", 16), ("expander64_p48", 1001)])
+def test_ell_kernel_sizes_and_widths(name, p, mode, gpu, oracle_mod, monkeypatch):
+    """The ELL low-degree kernel at ragged sizes (float4 / float2 / scalar paths by p), every chunk
+    count per wave (NIIDMIX_ELL_CH), bitwise the C oracle in exact mode (and the average-only flag),
+    within the tolerance in fast mode; the golden fixture's own x in the first columns."""
+    g = load_golden(name)
+    m = _mixer(g, gpu)
+    if m.ell is None:
+        pytest.skip("a row has more than 8 entries")
+    rng = np.random.default_rng(p)
+    xh = rng.standard_normal((m.n, p)).astype(np.float32)
+    k0 = min(p, g["x"].shape[1])
+    xh[:, :k0] = g["x"][:, :k0]
+    x = torch.from_numpy(xh).to(gpu)
+    ref = oracle_mod.mix_exact_c(xh, g["row_ptr"], g["col"], g["val"])
+    bound = oracle_mod.condition_bound(xh, g["row_ptr"], g["col"], g["val"])
+    for ch in ("1", "2", "4"):
+        monkeypatch.setenv("NIIDMIX_ELL_CH", ch)
+        y = m(x, kernel="ell-" + mode).cpu().numpy()
+        if mode == "exact":
+            assert oracle_mod.bitwise_equal(y, ref), ch
+        else:
+            ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+            assert ok, (ch, worst)
+    if mode == "exact":
+        ops = _ops()
+        out = torch.empty_like(x)
+        ops.mix_ell(x, m.e_col, m.e_val, m.e_len, out, m.ell, ops.EXACT | ops.AVERAGE_ONLY)
+        ref = oracle_mod.mix_exact_c(xh, g["row_ptr"], g["col"], g["val"], average_only=True)
+        assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref)
+
+
+def test_blocked_overlap_checks_use_each_block_stride(gpu):
+    """Column-blocked slabs whose block strides differ: out's block 1 IS x's block 1 (x's blocks
+    at 2R and 3R, out's at 0 and 3R).  The overlap checks measure each slab with its own block
+    stride, so the mixing op and the blocked gradient mean both refuse it (Jacobi, d_sgd.py:99-116;
+    the mean is out-of-place, d_sgd.py:19-45)."""
+    from niidmix import ops
+    g = load_golden("dcliques300_fc_p37")
+    m = _mixer(g, gpu)
+    rows, bc = 300, 1024
+    r_ = rows * bc
+    flat = torch.zeros(6 * r_, device=gpu)
+    x = flat[2 * r_:4 * r_].view(2, rows, bc)
+    out = torch.as_strided(flat, (2, rows, bc), (3 * r_, bc, 1))
+    assert out[1].data_ptr() == x[1].data_ptr()
+    with pytest.raises(RuntimeError, match="overlap"):
+        m.mix_blocked(x, out, 2 * bc)
+    seg_ptr = torch.tensor([0, 2], dtype=torch.int32, device=gpu)
+    seg_row = torch.tensor([0, 1], dtype=torch.int32, device=gpu)
+    with pytest.raises(RuntimeError, match="overlap"):
+        ops.grad_segment_mean_blocked(x, seg_ptr, seg_row, out, 2 * bc)
+    # disjoint slabs with different block strides are accepted
+    out_ok = torch.as_strided(flat, (2, rows, bc), (r_, bc, 1))[:, :, :]
+    out_ok = torch.zeros(3 * r_, device=gpu).as_strided((2, rows, bc), (int(1.5 * r_), bc, 1))
+    m.mix_blocked(x, out_ok, 2 * bc)

@@ -172,3 +172,37 @@ def test_striped_mixer_bigclique_blocked(gpu):
         assert torch.equal(sm.from_layout(ys), y_full[:, sm.c0:sm.c1]), r
         covered += sm.p_local
     assert covered == p
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("p", [1000, 4096])
+def test_local_sharded_round_c_abi(world, p, gpu, oracle_mod):
+    """The C-ABI sharded round (niidmix_mix_sharded_f32 via niidmix.shard.LocalShardedRound):
+    world 1 builds a real RCCL communicator (ncclCommInitAll over the one device, nothing to
+    exchange); worlds 2 and 3 put every shard on this GPU, so the halo exchange runs as
+    device-to-device copies (the same pack / exchange / per-shard CSR path as over RCCL).  Two
+    exact rounds are bitwise the oracle applied twice; a fast round is within the tolerance."""
+    from niidmix.shard import LocalShardedRound
+    g = load_golden("dcliques1000_fc_p64")
+    from niidmix.ops import csr_from_numpy
+    csr = csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    sr = LocalShardedRound(csr, g["cliques"], [gpu] * world, p)
+    assert sr.loopback == (world > 1)
+    if world > 1:
+        assert all(len(h["peer"]) > 0 for h in sr.host)
+    xh = torch.randn(1000, p, generator=torch.Generator().manual_seed(p + world))
+    sr.scatter(xh.to(gpu))
+    sr("exact")
+    sr("exact")
+    y = sr.gather().numpy()
+    ref = xh.numpy()
+    for _ in range(2):
+        ref = oracle_mod.mix_exact_c(ref, g["row_ptr"], g["col"], g["val"])
+    assert oracle_mod.bitwise_equal(y, ref)
+    sr.scatter(xh.to(gpu))
+    sr("fast")
+    yf = sr.gather().numpy()
+    r1 = oracle_mod.mix_exact_c(xh.numpy(), g["row_ptr"], g["col"], g["val"])
+    bound = oracle_mod.condition_bound(xh.numpy(), g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(yf, r1, bound, rtol=1e-5)
+    assert ok, worst

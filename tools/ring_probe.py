@@ -50,21 +50,28 @@ def main():
              m.val.data_ptr(), mode, strm)]
     t_raw = timed(lambda i: f(*args[i & 1]), a.iters)
     t_mixer = timed(lambda i: m(x, out=y, kernel="csr-fast") if i % 2 == 0 else m(y, out=x, kernel="csr-fast"), a.iters)
-    g = torch.cuda.CUDAGraph()
-    torch.cuda.synchronize()
-    with torch.cuda.graph(g):
-        for i in range(50):
-            if i % 2 == 0:
-                m(x, out=y, kernel="csr-fast")
-            else:
-                m(y, out=x, kernel="csr-fast")
-    t_graph = timed(lambda i: g.replay(), max(1, a.iters // 50)) / 50
+    t_graph = {}
+    for kern in ("csr-fast", "ell-fast", "csr-exact", "ell-exact"):
+        for ch in (["4", "2", "1"] if kern.startswith("ell") else [""]):
+            os.environ["NIIDMIX_ELL_CH"] = ch or "4"
+            g = torch.cuda.CUDAGraph()
+            m(x, out=y, kernel=kern)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                for i in range(50):
+                    if i % 2 == 0:
+                        m(x, out=y, kernel=kern)
+                    else:
+                        m(y, out=x, kernel=kern)
+            t_graph[kern + (f"/ch{ch}" if ch else "")] = timed(lambda i: g.replay(), max(1, a.iters // 50)) / 50
     numel = n * p - (n * p) % 4
     xa, ya = x.view(-1)[:numel], y.view(-1)[:numel]
     cp = _lib.lib.niidmix_stream_copy_f32
     t_copy = timed(lambda i: cp(xa.data_ptr(), ya.data_ptr(), numel, strm), a.iters)
-    print(f"ring100 N={n} P={p}: raw ctypes {t_raw:.2f} us  mixer {t_mixer:.2f} us  "
-          f"mixer in hipGraph {t_graph:.2f} us  stream copy {t_copy:.2f} us")
+    print(f"ring100 N={n} P={p}: raw ctypes csr {t_raw:.2f} us  mixer csr {t_mixer:.2f} us  "
+          f"stream copy {t_copy:.2f} us")
+    for k, v in t_graph.items():
+        print(f"  hipGraph {k}: {v:.2f} us per round")
 
 
 if __name__ == "__main__":
