@@ -397,8 +397,8 @@ def randomized_topology(nodes, params, rundir):
     """The next round's random graph (d_sgd.py:223-234: random_graph.generate_topology with the
     incremented topology-seed), built SPARSE: the edge lists by the restated generator
     (niidmix.generate.random_graph, same RNG order, hence the same graph) and the MH weights as a
-    CSR (topology.mh_csr, bit-identical to compute_weights) -- O(N k) weights instead of the dense
-    N x N matrix.  Every round the rundir gets topology.json (d_sgd.py:229-230), always readable
+    CSR (topology.mh_csr, bit-identical to compute_weights) -- O(N k) storage instead of the dense
+    N x N matrix (the diagonal keeps the reference's O(N^2) fp32 row sums, batched).  Every round the rundir gets topology.json (d_sgd.py:229-230), always readable
     by the reference's loader: up to NIIDMIX_DENSE_JSON_MAX nodes (default 1024) with the dense
     weights the reference writes, above it in the sparse form (niidmix.topology.sparse_json:
     'weights': [] + the CSR in topology.csr.npz), so the file never lags the graph the round used.

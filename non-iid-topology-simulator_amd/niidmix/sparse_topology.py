@@ -9,8 +9,9 @@ the weights as a CSR (topology.csr.npz) instead of a dense N x N matrix inside t
 Same arguments, defaults and params.json 'topology' section as the reference CLIs
 (tools/setup/topology/d_cliques/random_cliques.py:38-80, tools/setup/topology/random_graph.py:54-83),
 same graph (niidmix.generate restates the generators with the same RNG order; tests pin it), same
-Metropolis-Hastings weights bit for bit (niidmix.topology.mh_csr), but O(N * degree) memory and
-time for the weights: a 10 000-node d-cliques topology is ~12 MB of CSR instead of a ~1 GB JSON of
+Metropolis-Hastings weights bit for bit (niidmix.topology.mh_csr), but O(N * degree) memory for
+the weights (the fp32 diagonal is still reduced over dense rows, O(N^2) adds in batches, for bitwise
+equality with weights.py:25): a 10 000-node d-cliques topology is ~12 MB of CSR instead of a ~1 GB JSON of
 a dense matrix.  It also writes a topology.json that the reference's own loader reads unchanged
 (setup.topology.load, called by the unchanged run.py:92-93): 'edges' and 'cliques' as the
 reference writes them, 'weights': [] (an empty tensor once loaded) and 'weights-kind' /

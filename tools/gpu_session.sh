@@ -8,7 +8,7 @@ OUT=gpurun_out/${1:-session}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 rocm-smi --showproductname > "$OUT/rocm_smi.txt" 2>&1 || true
-timeout -k 10 900 python -m pytest tests -m gpu -q -rs > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rs --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
 if [ $rc -ge 2 ]; then exit $rc; fi
