@@ -859,13 +859,19 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
             else bad |= 1u << r;
         }
     }
-    while (bad) {                              // non-finite guard, per lane (see csr_refix)
-        const int r = __builtin_ctz(bad);
-        bad &= bad - 1;
-        const int64_t row = __shfl(d_rg, sl0 + r) & kRowMask;
-        float o[4];
-        csr_refix<4>(xc, ld_x, lo, true, row, csr_ptr, csr_col, csr_val, o);
-        stv_nt<4>(yc + row * ld_y + lo, o);
+    // non-finite guard, per lane (see csr_refix).  The slot loop is wave-uniform: __shfl (ds_bpermute)
+    // reads 0 from a lane that is not executing, so the row must be fetched with every lane active,
+    // not inside a loop over this lane's own `bad` bits.
+    if (__ballot(bad != 0u)) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int64_t row = __shfl(d_rg, sl0 + r) & kRowMask;
+            if ((bad >> r) & 1u) {
+                float o[4];
+                csr_refix<4>(xc, ld_x, lo, true, row, csr_ptr, csr_col, csr_val, o);
+                stv_nt<4>(yc + row * ld_y + lo, o);
+            }
+        }
     }
 }
 

@@ -537,7 +537,21 @@ class Mixer:
         if self.tlds is None:
             return
         lp = self.tlds
+        # segment loop (RT 16): runs of consecutive LDS slots read at immediate offsets
+        # (niidmix.tile.build_tile_segments); NIIDMIX_TLDS_SEG=0 keeps the per-position loop
+        ts = None
+        if lp.tile.rt == 16 and os.environ.get("NIIDMIX_TLDS_SEG", "1") != "0":
+            ts = self._hosted(("tseg", lp.tile.rt), lambda: build_tile_segments(lp))
+        # unbound: `self` may be the lazy builder's scratch object, whose attribute lookups (bound
+        # methods included) fall through to the Mixer
+        Mixer.set_tile_lds_plan(self, lp, ts)
+
+    def set_tile_lds_plan(self, lp, ts=None):
+        """Upload an LDS tile plan (niidmix.tile.build_tile_lds_plan) and its segments (or None:
+        the per-position loop) to this Mixer's device."""
+        dev = self.device
         tp = lp.tile
+        self.tlds = lp
         self.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
         self.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
         self.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
@@ -548,15 +562,12 @@ class Mixer:
         self.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
         self.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
         self.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
-        # segment loop (RT 16): runs of consecutive LDS slots read at immediate offsets
-        # (niidmix.tile.build_tile_segments); NIIDMIX_TLDS_SEG=0 keeps the per-position loop
-        self.tseg = None
-        if tp.rt == 16 and os.environ.get("NIIDMIX_TLDS_SEG", "1") != "0":
-            self.tseg = self._hosted(("tseg", tp.rt), lambda: build_tile_segments(lp))
-        if self.tseg is not None:
-            self.s_seg_ptr = torch.from_numpy(self.tseg.seg_ptr).to(dev)
-            self.s_seg = torch.from_numpy(np.ascontiguousarray(self.tseg.seg)).to(dev)
-            self.s_seg_w = torch.from_numpy(self.tseg.seg_w).to(dev)
+        self.tseg = ts
+        if ts is not None:
+            # flat 1-D device arrays: seg [S*4] int32 (16-B rows), seg_w [T*2] fp32
+            self.s_seg_ptr = torch.from_numpy(ts.seg_ptr).to(dev)
+            self.s_seg = torch.from_numpy(np.ascontiguousarray(ts.seg).reshape(-1)).to(dev)
+            self.s_seg_w = torch.from_numpy(np.ascontiguousarray(ts.seg_w).reshape(-1)).to(dev)
 
     def _build_ell(self):
         lay = self._hosted("ell", lambda: ell_layout(self.csr))

@@ -110,23 +110,7 @@ def _tile_lds_mixer(g, dev, rt):
     lp, why = tile.build_tile_lds_plan(m.csr, cl, rt)
     if lp is None:
         pytest.skip(why)
-    tp = lp.tile
-    m.tlds = lp
-    m.l_sub_ptr = torch.from_numpy(tp.sub_ptr).to(dev)
-    m.l_sub_rows = torch.from_numpy(tp.sub_rows).to(dev)
-    m.l_sub_slot = torch.from_numpy(lp.sub_slot).to(dev)
-    m.l_sub_wself = torch.from_numpy(tp.sub_wself).to(dev)
-    m.l_pos_slot = torch.from_numpy(lp.pos_slot).to(dev)
-    m.l_pos_mask = torch.from_numpy(tp.pos_mask.view(np.int32)).to(dev)
-    m.l_pos_w = torch.from_numpy(tp.pos_w).to(dev)
-    m.l_grp_tile_ptr = torch.from_numpy(lp.grp_tile_ptr).to(dev)
-    m.l_grp_src_ptr = torch.from_numpy(lp.grp_src_ptr).to(dev)
-    m.l_grp_src_rows = torch.from_numpy(lp.grp_src_rows).to(dev)
-    m.tseg = tile.build_tile_segments(lp) if rt == 16 else None
-    if m.tseg is not None:
-        m.s_seg_ptr = torch.from_numpy(m.tseg.seg_ptr).to(dev)
-        m.s_seg = torch.from_numpy(np.ascontiguousarray(m.tseg.seg)).to(dev)
-        m.s_seg_w = torch.from_numpy(m.tseg.seg_w).to(dev)
+    m.set_tile_lds_plan(lp, tile.build_tile_segments(lp) if rt == 16 else None)
     return m
 
 
