@@ -188,6 +188,25 @@ def e2e_rounds(mixer, n, p, dev, rounds=3):
             ts.append(runner.last_timing["round_s"])
         t = float(np.median(ts))
         res[mode] = {"round_ms": round(t * 1e3, 2), "GBs": round(n * p * 4 / t / 1e9, 1)}
+    # the 'sample' topology's round (d_sgd.py:235-250) as the drop-in runs it (d_sgd.sample_average:
+    # SampleAverage streamed over the same pinned slab): average of k active rows, then
+    # update_models of every row; k = n / 10 rows drawn like get_sample's Random(42)
+    from random import Random
+    from niidmix.slab import SampleAverage
+    k = max(1, n // 10)
+    active = Random(42).sample(range(n), k)
+    op = SampleAverage(dev)
+    op.set_active(active, [1 / k] * k)
+    srun = SlabMixer(op, n, p, dev, window=runner.window)
+    srun.mix(host, mode="exact")
+    ts = []
+    for _ in range(rounds):
+        srun.mix(host, mode="exact", timing=True)
+        ts.append(srun.last_timing["round_s"])
+    t = float(np.median(ts))
+    res["sample"] = {"round_ms": round(t * 1e3, 2), "GBs": round(n * p * 4 / t / 1e9, 1),
+                     "active_rows": k}
+    del srun
     # PCIe reference: one plain pinned H2D and D2H of the whole slab
     d = torch.empty((n, p), dtype=torch.float32, device=dev)
     torch.cuda.synchronize()

@@ -687,7 +687,7 @@ __device__ __forceinline__ const float *qrow(const float *base, int row, int64_t
         return base + (int64_t)row * ld + lo;
 }
 
-template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32>
+template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32, bool LATE>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique_q(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
@@ -757,10 +757,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         ldv<4>(qrow<OFF32>(xc, rg < 0 ? 0 : rg & kRowMask, ld_x, lo), v[r]);
     }
     float ga[NA][4];
+    if constexpr (!LATE) {
 #pragma unroll
-    for (int r = 0; r < NA; ++r) {
-        const int rc = __shfl(d_rc, sl0 + r);
-        ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r]);
+        for (int r = 0; r < NA; ++r) {
+            const int rc = __shfl(d_rc, sl0 + r);
+            ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r]);
+        }
     }
     // every load above is issued before any use below (the scheduler would otherwise fuse the
     // per-slot loops and serialise the loads slot by slot under the 64-VGPR budget)
@@ -785,16 +787,32 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[r][e] *= a;
     }
-#pragma unroll
-    for (int r = 0; r < NA; ++r) {
-        const bool has = __shfl(d_rc, sl0 + r) >= 0;
-        const float w = __shfl(d_rv, sl0 + r);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
+    if constexpr (LATE) {
+        // LATE: every gateway gather waits until after the cross-wave group sums, so the chunk's
+        // other items (in flight together on this XCD) have loaded their member rows into L2 first
+        __syncthreads();
+        if (wave < G) {
+            float4 a = red[wave][0][lane];
+#pragma unroll 4
+            for (int w = 1; w < WAVES; ++w) {
+                const float4 b = red[wave][w][lane];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            tot[wave][lane] = a;
+        }
     }
-    // gathers of slots [NA, RPW) in batches of NA, in ga's registers
+    // gathers of slots [LATE ? 0 : NA, RPW) in batches of NA, in ga's registers
+    if constexpr (!LATE) {
 #pragma unroll
-    for (int b0 = NA; b0 < RPW; b0 += NA) {
+        for (int r = 0; r < NA; ++r) {
+            const bool has = __shfl(d_rc, sl0 + r) >= 0;
+            const float w = __shfl(d_rv, sl0 + r);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
+        }
+    }
+#pragma unroll
+    for (int b0 = LATE ? 0 : NA; b0 < RPW; b0 += NA) {
 #pragma unroll
         for (int r = b0; r < RPW && r < b0 + NA; ++r) {
             const int rc = __shfl(d_rc, sl0 + r);
@@ -826,16 +844,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
             }
         }
     }
-    // 3. group sums across waves
-    __syncthreads();
-    if (wave < G) {
-        float4 a = red[wave][0][lane];
+    // 3. group sums across waves (LATE: reduced above, before the gathers)
+    if constexpr (!LATE) {
+        __syncthreads();
+        if (wave < G) {
+            float4 a = red[wave][0][lane];
 #pragma unroll 4
-        for (int w = 1; w < WAVES; ++w) {
-            const float4 b = red[wave][w][lane];
-            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            for (int w = 1; w < WAVES; ++w) {
+                const float4 b = red[wave][w][lane];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            tot[wave][lane] = a;
         }
-        tot[wave][lane] = a;
     }
     __syncthreads();
     float sg[G][4];
@@ -1584,28 +1604,40 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     else NIIDMIX_TLDS_RUN(NIIDMIX_UPD_FAST);
 }
 
-// The RT = 16 position loop over one SEGMENT (niidmix.tile.build_tile_segments): positions
-// i = 0 .. len-1 read consecutive LDS slots, so position i's row sits at one base address +
-// i * RB bytes -- an immediate offset, no per-position descriptor, no v_readlane; its weight is the
-// tile's w0 or w1 (bit i of wsel, picked by SALU) and it is taken by every row, or (bit i of skip)
-// by all rows but the next one of the segment's skipped rows r0, r0 + 1, ... (saved, updated with
-// the others, restored: bit-exact).  The row two positions ahead is read while one is applied;
-// the segment's LDS allocation holds two spare rows for the reads past its end.
-// Scratch registers are asm operands (compiler-allocated), not fixed ones, so that the values the
-// kernel keeps live across the segment loop can share the low VGPRs: x0..x3 the rotating row pairs,
-// pr the product, sv0/sv1 the saved skipped row, va the read address.
+// The RT = 16 segment walker (niidmix.tile.build_tile_segments): ONE asm block walks up to 64 of a
+// tile's segments, so the accumulator tuple stays pinned in v[32:63] from the first segment to the
+// last (one asm statement per segment let the compiler keep the tuple in other registers between
+// them and copy all 16 pairs in and out around every segment: 32 v_mov per segment, ~30 % of the
+// kernel's VALU instructions).  Segment j's descriptor words sit in lane j of dx / dy / dz.
+//  * a RUN (bit 30 of dx clear): dx = first slot | length << 12 | first skipped row << 20,
+//    dy = weight-select bits, dz = skip bits.  Positions i = 0 .. len-1 read consecutive LDS slots,
+//    so position i's row sits at one base address + i * RB bytes -- an immediate offset, no
+//    per-position descriptor; its weight is the tile's w0 or w1 (bit i of dy, picked by SALU) and it
+//    is taken by every row, or (bit i of dz) by all rows but the next one of the run's skipped rows
+//    r0, r0 + 1, ... (saved, updated with the others, restored: bit-exact).  The row two positions
+//    ahead is read while one is applied; the LDS stage holds two spare rows for the reads past a
+//    run's end (those reads land before the next run's own reads: LDS returns in order).
+//  * a MASKED position (bit 30 set): dx = slot | 1 << 30, dy = the rows that take it, dz = its
+//    weight (fp32 bits) -- a row taking a gateway's inter-clique edge alone, a source two rows order
+//    differently, or one weight class of a position whose rows carry different weights (split by
+//    weight, each row still takes it once, in its own order).  Each of its rows is reached by
+//    GPR-index mode (s_set_gpr_idx).
+// Fixed scratch SGPRs: s38 run length, s39 LDS address, s40 segment index, s41 dx, s42 dy (masked:
+// the remaining rows), s43 dz, s44 weight, s46 skipped row * 2 / row index, s47 position.  VGPR
+// scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
+// saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
 #define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
-    "s_bitcmp1_b32 %[wsel], s47\n\t"                                                                 \
+    "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
     "s_cselect_b32 s44, %[w1], %[w0]\n\t"                                                            \
-    "s_bitcmp1_b32 %[skip], s47\n\t"                                                                 \
+    "s_bitcmp1_b32 s43, s47\n\t"                                                                     \
     "s_waitcnt lgkmcnt(2)\n\t"                                                                       \
     "s_cbranch_scc1 .Lseg_skip" K "_%=\n\t" UPD(XD)                                                 \
     "\n.Lseg_back" K "_%=:\n\t"                                                                     \
     "s_add_u32 s47, s47, 1\n\t"                                                                      \
-    "s_cmp_ge_u32 s47, %[len]\n\t"                                                                   \
-    "s_cbranch_scc1 .Lseg_done_%=\n\t"
+    "s_cmp_ge_u32 s47, s38\n\t"                                                                      \
+    "s_cbranch_scc1 .Lw_next_%=\n\t"
 #define NIIDMIX_SEG_SKIPBLK(XD, K, UPD)                                                              \
     "\n.Lseg_skip" K "_%=:\n\t"                                                                     \
     "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
@@ -1618,12 +1650,54 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     "s_set_gpr_idx_off\n\t"                                                                          \
     "s_add_u32 s46, s46, 2\n\t"                                                                      \
     "s_branch .Lseg_back" K "_%=\n\t"
-#define NIIDMIX_SEG_RUN(UPD)                                                                         \
-    asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"                                             \
-                 "ds_read_b64 %[x0], %[va]\n\t"                                                     \
-                 "ds_read_b64 %[x1], %[va] offset:%[o1]\n\t"                                        \
-                 "s_mov_b32 s47, 0\n\t"                                                              \
-                 "s_lshl_b32 s46, %[r0], 1\n"                                                        \
+// a masked position's per-row update: exact adds the product formed once, fast fmas the row
+#define NIIDMIX_MSK_EXACT                                                                            \
+    "v_mul_f32 %[q0], s43, %[q0]\n\t"                                                                \
+    "v_mul_f32 %[q1], s43, %[q1]\n"                                                                  \
+    ".Lmsk_loop_%=:\n\t"                                                                             \
+    "s_ff1_i32_b32 s46, s42\n\t"                                                                     \
+    "s_cmp_lt_i32 s46, 0\n\t"                                                                        \
+    "s_cbranch_scc1 .Lw_next_%=\n\t"                                                                 \
+    "s_bitset0_b32 s42, s46\n\t"                                                                     \
+    "s_lshl_b32 s46, s46, 1\n\t"                                                                     \
+    "s_set_gpr_idx_on s46, gpr_idx(SRC0,DST)\n\t"                                                   \
+    "v_add_f32 v32, v32, %[q0]\n\t"                                                                  \
+    "v_add_f32 v33, v33, %[q1]\n\t"                                                                  \
+    "s_set_gpr_idx_off\n\t"                                                                          \
+    "s_branch .Lmsk_loop_%=\n\t"
+#define NIIDMIX_MSK_FAST                                                                             \
+    ".Lmsk_loop_%=:\n\t"                                                                             \
+    "s_ff1_i32_b32 s46, s42\n\t"                                                                     \
+    "s_cmp_lt_i32 s46, 0\n\t"                                                                        \
+    "s_cbranch_scc1 .Lw_next_%=\n\t"                                                                 \
+    "s_bitset0_b32 s42, s46\n\t"                                                                     \
+    "s_lshl_b32 s46, s46, 1\n\t"                                                                     \
+    "s_set_gpr_idx_on s46, gpr_idx(SRC2,DST)\n\t"                                                   \
+    "v_fma_f32 v32, %[q0], s43, v32\n\t"                                                             \
+    "v_fma_f32 v33, %[q1], s43, v33\n\t"                                                             \
+    "s_set_gpr_idx_off\n\t"                                                                          \
+    "s_branch .Lmsk_loop_%=\n\t"
+#define NIIDMIX_SEG_WALK(UPD, MSK)                                                                   \
+    asm volatile("s_mov_b32 s40, 0\n"                                                                \
+                 ".Lw_next_%=:\n\t"                                                                  \
+                 "s_cmp_ge_u32 s40, %[cnt]\n\t"                                                      \
+                 "s_cbranch_scc1 .Lw_end_%=\n\t"                                                     \
+                 "v_readlane_b32 s41, %[dx], s40\n\t"                                                \
+                 "v_readlane_b32 s42, %[dy], s40\n\t"                                                \
+                 "v_readlane_b32 s43, %[dz], s40\n\t"                                                \
+                 "s_add_u32 s40, s40, 1\n\t"                                                         \
+                 "s_and_b32 s39, s41, 0xfff\n\t"                                                     \
+                 "s_mul_i32 s39, s39, %[o1]\n\t"                                                     \
+                 "s_add_u32 s39, s39, %[base]\n\t"                                                   \
+                 "v_add_u32 %[va], s39, %[l8]\n\t"                                                   \
+                 "s_bitcmp1_b32 s41, 30\n\t"                                                         \
+                 "s_cbranch_scc1 .Lw_masked_%=\n\t"                                                  \
+                 "ds_read_b64 %[x0], %[va]\n\t"                                                      \
+                 "ds_read_b64 %[x1], %[va] offset:%[o1]\n\t"                                         \
+                 "s_bfe_u32 s38, s41, 0x8000c\n\t"                                                   \
+                 "s_bfe_u32 s46, s41, 0x80014\n\t"                                                   \
+                 "s_lshl_b32 s46, s46, 1\n\t"                                                        \
+                 "s_mov_b32 s47, 0\n"                                                                \
                  ".Lseg_loop_%=:\n\t"                                                                \
                  NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", "0", UPD)                                    \
                  NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", "1", UPD)                                    \
@@ -1635,79 +1709,30 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  NIIDMIX_SEG_SKIPBLK("%[x1]", "1", UPD)                                               \
                  NIIDMIX_SEG_SKIPBLK("%[x2]", "2", UPD)                                               \
                  NIIDMIX_SEG_SKIPBLK("%[x3]", "3", UPD)                                               \
-                 "\n.Lseg_done_%=:\n\t"                                                             \
+                 "\n.Lw_masked_%=:\n\t"                                                              \
+                 "ds_read_b32 %[q0], %[va]\n\t"                                                      \
+                 "ds_read_b32 %[q1], %[va] offset:4\n\t"                                             \
+                 "s_waitcnt lgkmcnt(0)\n\t"                                                          \
+                 MSK                                                                                 \
+                 "\n.Lw_end_%=:\n\t"                                                                 \
                  "s_waitcnt lgkmcnt(0)"                                                              \
                  : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2),             \
                    [x3] "=&v"(x3), [pr] "=&v"(pr), [sv0] "=&v"(sv0), [sv1] "=&v"(sv1),              \
-                   [va] "=&v"(va)                                                                   \
-                 : [addr] "s"(addr), [len] "s"(len), [wsel] "s"(wsel), [skip] "s"(skip),             \
-                   [r0] "s"(r0), [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),            \
+                   [q0] "=&v"(q0), [q1] "=&v"(q1), [va] "=&v"(va)                                   \
+                 : [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz), [cnt] "s"(cnt), [base] "s"(base),       \
+                   [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),                          \
                    [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB)             \
-                 : "s44", "s45", "s46", "s47", "m0", "scc", "memory")
+                 : "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "m0", "scc", \
+                   "memory")
 template <bool EXACT, int RB>
-__device__ __forceinline__ void tlds16_seg(Acc16 &acc, int addr, int len, uint32_t wsel,
-                                           uint32_t skip, int r0, int w0, int w1, int lane8) {
+__device__ __forceinline__ void tlds16_walk(Acc16 &acc, int dx, int dy, int dz, int cnt, int base,
+                                            int w0, int w1, int lane8) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
     uint64_t x0, x1, x2, x3, pr;
-    uint32_t sv0, sv1, va;
-    if constexpr (EXACT) NIIDMIX_SEG_RUN(NIIDMIX_SEG_UPD_EXACT);
-    else NIIDMIX_SEG_RUN(NIIDMIX_UPD_FAST);
+    uint32_t sv0, sv1, q0, q1, va;
+    if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
+    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
     (void)pr;
-}
-
-// One position taken by the rows of `mask` with the uniform weight w (a segment's MASKED entry: a
-// row taking a gateway's inter-clique edge alone, a source two rows order differently, or one
-// weight class of a position whose rows carry different weights -- split by weight, each row still
-// takes it once, in its own order).  Each row is reached by GPR-index mode (s_set_gpr_idx), the
-// accumulator tuple stays pinned in v[32:63].
-template <bool EXACT>
-__device__ __forceinline__ void tlds16_masked(Acc16 &acc, int addr, uint32_t mask, int w, int lane8) {
-    uint32_t x0, x1, va, m;
-    if constexpr (EXACT) {
-        asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"
-                     "ds_read_b32 %[x0], %[va]\n\t"
-                     "ds_read_b32 %[x1], %[va] offset:4\n\t"
-                     "s_mov_b32 %[m], %[mask]\n\t"
-                     "s_waitcnt lgkmcnt(0)\n\t"
-                     "v_mul_f32 %[x0], %[w], %[x0]\n\t"
-                     "v_mul_f32 %[x1], %[w], %[x1]\n"
-                     ".Lmsk_loop_%=:\n\t"
-                     "s_ff1_i32_b32 s46, %[m]\n\t"
-                     "s_cmp_lt_i32 s46, 0\n\t"
-                     "s_cbranch_scc1 .Lmsk_done_%=\n\t"
-                     "s_bitset0_b32 %[m], s46\n\t"
-                     "s_lshl_b32 s46, s46, 1\n\t"
-                     "s_set_gpr_idx_on s46, gpr_idx(SRC0,DST)\n\t"
-                     "v_add_f32 v32, v32, %[x0]\n\t"
-                     "v_add_f32 v33, v33, %[x1]\n\t"
-                     "s_set_gpr_idx_off\n\t"
-                     "s_branch .Lmsk_loop_%=\n"
-                     ".Lmsk_done_%=:"
-                     : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [va] "=&v"(va), [m] "=&s"(m)
-                     : [addr] "s"(addr), [mask] "s"(mask), [w] "s"(w), [l8] "v"(lane8)
-                     : "s46", "m0", "scc", "memory");
-    } else {
-        asm volatile("v_add_u32 %[va], %[addr], %[l8]\n\t"
-                     "ds_read_b32 %[x0], %[va]\n\t"
-                     "ds_read_b32 %[x1], %[va] offset:4\n\t"
-                     "s_mov_b32 %[m], %[mask]\n\t"
-                     "s_waitcnt lgkmcnt(0)\n"
-                     ".Lmsk_loop_%=:\n\t"
-                     "s_ff1_i32_b32 s46, %[m]\n\t"
-                     "s_cmp_lt_i32 s46, 0\n\t"
-                     "s_cbranch_scc1 .Lmsk_done_%=\n\t"
-                     "s_bitset0_b32 %[m], s46\n\t"
-                     "s_lshl_b32 s46, s46, 1\n\t"
-                     "s_set_gpr_idx_on s46, gpr_idx(SRC2,DST)\n\t"
-                     "v_fma_f32 v32, %[x0], %[w], v32\n\t"
-                     "v_fma_f32 v33, %[x1], %[w], v33\n\t"
-                     "s_set_gpr_idx_off\n\t"
-                     "s_branch .Lmsk_loop_%=\n"
-                     ".Lmsk_done_%=:"
-                     : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [va] "=&v"(va), [m] "=&s"(m)
-                     : [addr] "s"(addr), [mask] "s"(mask), [w] "s"(w), [l8] "v"(lane8)
-                     : "s46", "m0", "scc", "memory");
-    }
 }
 
 // Apply op(acc_row, r) to the rows of the wave-uniform mask m.  No per-row select: on gfx950 a lane
@@ -1743,11 +1768,23 @@ __device__ __forceinline__ void apply_mask(TileAcc<RT> &acc, uint32_t m, Op op) 
 }
 
 // Time-split switch for tuning builds only (tools/tlds_split.sh builds variant libraries): 1 skips
-// the position loop, 2 skips the staging; 3-5 strip the position loop down (3: every position full
+// the position / segment loop, 2 skips the staging (the segment loop still runs); 3-5 strip the position loop down (3: every position full
 // and uniform, 4: no product either, 5: no adds).  Product builds leave it 0.
 #ifndef NIIDMIX_TLDS_SPLIT
 #define NIIDMIX_TLDS_SPLIT 0
 #endif
+// Stage by LDS-DMA (1) or through registers (0; tuning A/B builds only).
+#ifndef NIIDMIX_TLDS_GLDS
+#define NIIDMIX_TLDS_GLDS 1
+#endif
+// LDS bytes past the staged rows: the LDS-DMA staging writes whole 1 KiB wave-instructions, the last
+// one up to 1008 B past the group's rows; the segment loop's two spare rows absorb part of that
+// (an LDS allocation counts in 512-B granules: 1000-node d-cliques at 120 columns keep three
+// blocks per CU only with <= 480 B more than the 111 rows)
+inline size_t tlds_slack(bool seg, int cw) {
+    const size_t spare = seg ? 2 * (size_t)cw * sizeof(float) : 0;
+    return NIIDMIX_TLDS_GLDS && spare < 1024 ? 1024 - spare : 0;
+}
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
 template <bool EXACT, int RT, int SV, int RS, bool SEG>
@@ -1783,6 +1820,49 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const int s0 = grp_src_ptr[grp], ns = grp_src_ptr[grp + 1] - s0;
         const int total = ns * PPR;
         float *st = lds_tile;
+        if constexpr (SV == 4 && NIIDMIX_TLDS_GLDS) {
+            // LDS-DMA (global_load_lds_dwordx4): piece i of the stage lands at byte 16 i, so one
+            // wave-instruction's 64 pieces are the lane-linear 1 KiB the instruction writes; the
+            // per-lane source address gathers the rows.  The pieces of up to NB wave-instructions per
+            // wave are in flight at once, with no VGPR round trip; __syncthreads() below waits for
+            // them (vmcnt(0)).  Their row indices are loaded first, a batch at a time: hipcc waits
+            // vmcnt(0) at the first use of a plain load's result while an LDS-DMA is in flight, so an
+            // index load between two DMAs would drain the first.
+            typedef __attribute__((address_space(3))) void lds_void;
+            typedef __attribute__((address_space(1))) void glb_void;
+            constexpr int NB = 8;
+            const int step = n_waves * kWave;
+            for (int b0 = wave * kWave; b0 < total; b0 += NB * step) {
+                int rowi[NB];
+#pragma unroll
+                for (int u = 0; u < NB; ++u) {
+                    const int i = b0 + u * step + lane;
+                    rowi[u] = grp_src_rows[s0 + (i < total ? i : total - 1) / PPR];
+                }
+                const float *src[NB];
+#pragma unroll
+                for (int u = 0; u < NB; ++u) {
+                    const int i = b0 + u * step + lane;
+                    const int ii = i < total ? i : total - 1;       // lanes past the stage: a valid
+                    const int piece = ii - (ii / PPR) * PPR;        // source; they land in the slack
+                    const int64_t c = c0 + (int64_t)piece * 4;
+                    const int64_t cc = c < p ? c : c0;              // columns past p: any valid data
+                    src[u] = x + (int64_t)rowi[u] * ld_x + cc;
+                }
+                // every index consumed before the first DMA: the empty asm uses all addresses
+                // here, so no index load sinks between two DMAs (where it would cost a vmcnt(0))
+                asm volatile("" ::"v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3]), "v"(src[4]),
+                             "v"(src[5]), "v"(src[6]), "v"(src[7]));
+                static_assert(NB == 8, "the asm above names NB addresses");
+#pragma unroll
+                for (int u = 0; u < NB; ++u) {
+                    const int i0 = b0 + u * step;                   // wave-uniform: whole 1 KiB
+                    if (i0 < total)                                 // pieces (tlds_slack covers the
+                        __builtin_amdgcn_global_load_lds(           // last one's overhang)
+                            (glb_void *)src[u], (lds_void *)(st + 4 * i0), 16, 0, 0);
+                }
+            }
+        } else
         for (int i0 = 0; i0 < total; i0 += 4 * (int)blockDim.x) {
             float v[4][SV];
             int at[4];
@@ -1829,7 +1909,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
             acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
         }
-        if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && NIIDMIX_TLDS_SPLIT == 0) {
+        if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && (NIIDMIX_TLDS_SPLIT == 0 || NIIDMIX_TLDS_SPLIT == 2)) {
             {                                                            // segment loop (tile.py)
                 const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
                 const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
@@ -1840,20 +1920,8 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     // y = the rows that take it, z = its weight (fp32 bits)
                     const int cnt = sb1 - sb < 64 ? sb1 - sb : 64;
                     const int4 da = reinterpret_cast<const int4 *>(seg)[sb + (lane < cnt ? lane : cnt - 1)];
-                    for (int j = 0; j < cnt; ++j) {
-                        const int hd = __builtin_amdgcn_readlane(da.x, j);
-                        if (hd & (1 << 30)) {                            // one MASKED position
-                            tlds16_masked<EXACT>(acc.v[0], (int)lds_base + (hd & 0xfff) * rs * (int)sizeof(f2),
-                                                 (uint32_t)__builtin_amdgcn_readlane(da.y, j),
-                                                 __builtin_amdgcn_readlane(da.z, j), lane8);
-                            continue;
-                        }
-                        const int s0 = hd & 0xfff, ln = (hd >> 12) & 0xff, r0 = (hd >> 20) & 0xff;
-                        const uint32_t wsel = (uint32_t)__builtin_amdgcn_readlane(da.y, j);
-                        const uint32_t skp = (uint32_t)__builtin_amdgcn_readlane(da.z, j);
-                        tlds16_seg<EXACT, rs * (int)sizeof(f2)>(acc.v[0], (int)lds_base + s0 * rs * (int)sizeof(f2),
-                                                               ln, wsel, skp, r0, w0, w1, lane8);
-                    }
+                    tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base,
+                                                             w0, w1, lane8);
                 }
                 goto tile_epilogue;
             }
@@ -2346,9 +2414,14 @@ int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
     // 32-bit row offsets when every block (column-blocked slabs) spans < 4 GiB
     const bool off32 = bg.bc_shift < 62 && bg.bs_x * 4 <= (int64_t)0xffffffffLL &&
                        bg.bs_y * 4 <= (int64_t)0xffffffffLL;
-#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
-    if (off32) NIIDMIX_CQ(true); else NIIDMIX_CQ(false);
+#define NIIDMIX_CQ(O) if (late) NIIDMIX_CQL(O, true); else NIIDMIX_CQL(O, false)
+#define NIIDMIX_CQL(O, L) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O, L>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
+    // NIIDMIX_CLIQUE_QLATE=1: gateway gathers after the group sums (A/B)
+    const char *le = getenv("NIIDMIX_CLIQUE_QLATE");
+    const bool late = le && atoi(le) == 1;
+    if (off32) { NIIDMIX_CQ(true); } else { NIIDMIX_CQ(false); }
 #undef NIIDMIX_CQ
+#undef NIIDMIX_CQL
     return check_launch("k_mix_clique_q");
 }
 
@@ -2868,7 +2941,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const int stage_rows = plan->max_src + (seg ? 2 : 0);
     if (plan->rt == 16) {
         auto blocks = [&](int c) {
-            const size_t per = (size_t)stage_rows * c * sizeof(float);
+            const size_t per = (size_t)stage_rows * c * sizeof(float) + tlds_slack(seg, c);
             const size_t b = per ? lds_cu / per : 3;
             return (int)(b < 3 ? b : 3);
         };
@@ -2883,7 +2956,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const int64_t n_chunks = (p + cw - 1) / cw;
     const int64_t n_items = (int64_t)plan->n_grp * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
-    const size_t lds = (size_t)stage_rows * cw * sizeof(float);
+    const size_t lds = (size_t)stage_rows * cw * sizeof(float) + tlds_slack(seg, cw);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
 #define NIIDMIX_TLDS(E, R, V) do { \
         auto kfn = seg ? (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16)>) \
