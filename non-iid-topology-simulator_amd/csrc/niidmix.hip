@@ -687,7 +687,7 @@ __device__ __forceinline__ const float *qrow(const float *base, int row, int64_t
         return base + (int64_t)row * ld + lo;
 }
 
-template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32, bool LATE>
+template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique_q(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     int64_t n_items, int cpb_shift, int64_t bs_x, int64_t bs_y,
     const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
     const float *__restrict__ csr_val) {
-    static_assert(Q * RPW <= 64 && (Q == 1 || Q == 2 || Q == 4), "descriptor lanes");
+    static_assert(Q * RPW <= 64 && (Q == 1 || Q == 2 || Q == 4 || Q == 8), "descriptor lanes");
     constexpr int LQ = 64 / Q;                 // lanes per clique
     constexpr int64_t CW = 4 * LQ;             // columns per item
     constexpr int NA = GA;                     // gateway gathers in flight per batch (the first
@@ -757,12 +757,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
         ldv<4>(qrow<OFF32>(xc, rg < 0 ? 0 : rg & kRowMask, ld_x, lo), v[r]);
     }
     float ga[NA][4];
-    if constexpr (!LATE) {
 #pragma unroll
-        for (int r = 0; r < NA; ++r) {
-            const int rc = __shfl(d_rc, sl0 + r);
-            ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r]);
-        }
+    for (int r = 0; r < NA; ++r) {
+        const int rc = __shfl(d_rc, sl0 + r);
+        ldv<4>(qrow<OFF32>(xc, rc < 0 ? 0 : rc, ld_x, lo), ga[r]);
     }
     // every load above is issued before any use below (the scheduler would otherwise fuse the
     // per-slot loops and serialise the loads slot by slot under the 64-VGPR budget)
@@ -787,32 +785,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[r][e] *= a;
     }
-    if constexpr (LATE) {
-        // LATE: every gateway gather waits until after the cross-wave group sums, so the chunk's
-        // other items (in flight together on this XCD) have loaded their member rows into L2 first
-        __syncthreads();
-        if (wave < G) {
-            float4 a = red[wave][0][lane];
-#pragma unroll 4
-            for (int w = 1; w < WAVES; ++w) {
-                const float4 b = red[wave][w][lane];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-            }
-            tot[wave][lane] = a;
-        }
+#pragma unroll
+    for (int r = 0; r < NA; ++r) {
+        const bool has = __shfl(d_rc, sl0 + r) >= 0;
+        const float w = __shfl(d_rv, sl0 + r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
     }
-    // gathers of slots [LATE ? 0 : NA, RPW) in batches of NA, in ga's registers
-    if constexpr (!LATE) {
+    // gathers of slots [NA, RPW) in batches of NA, in ga's registers (gathering them all after the
+    // group sums instead -- so the chunk's other items had loaded their rows into L2 first --
+    // measured slower: 18.1 vs 15.5 ms at 10 000 nodes, with register spills)
 #pragma unroll
-        for (int r = 0; r < NA; ++r) {
-            const bool has = __shfl(d_rc, sl0 + r) >= 0;
-            const float w = __shfl(d_rv, sl0 + r);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
-        }
-    }
-#pragma unroll
-    for (int b0 = LATE ? 0 : NA; b0 < RPW; b0 += NA) {
+    for (int b0 = NA; b0 < RPW; b0 += NA) {
 #pragma unroll
         for (int r = b0; r < RPW && r < b0 + NA; ++r) {
             const int rc = __shfl(d_rc, sl0 + r);
@@ -844,18 +828,16 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
             }
         }
     }
-    // 3. group sums across waves (LATE: reduced above, before the gathers)
-    if constexpr (!LATE) {
-        __syncthreads();
-        if (wave < G) {
-            float4 a = red[wave][0][lane];
+    // 3. group sums across waves
+    __syncthreads();
+    if (wave < G) {
+        float4 a = red[wave][0][lane];
 #pragma unroll 4
-            for (int w = 1; w < WAVES; ++w) {
-                const float4 b = red[wave][w][lane];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-            }
-            tot[wave][lane] = a;
+        for (int w = 1; w < WAVES; ++w) {
+            const float4 b = red[wave][w][lane];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
         }
+        tot[wave][lane] = a;
     }
     __syncthreads();
     float sg[G][4];
@@ -2401,38 +2383,34 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 // of <= 112 members).  Chosen when a 256-column chunk of all member rows (n_members KB) would not
 // fit an XCD's L2; NIIDMIX_CLIQUE_Q=1 disables it, =4 forces it (A/B).
 constexpr int64_t kQRowsMin = 4096;
-template <int G, int W, int R, int OCC, int GA>
+template <int G, int W, int R, int OCC, int GA, int Q>
 int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                     const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
-    constexpr int Q = 4;
     constexpr int64_t CW = 4 * (64 / Q);
+    constexpr int CW_SHIFT = Q == 8 ? 5 : 6;
+    if (bg.bc_shift < CW_SHIFT) return set_error(NIIDMIX_EINVAL, "%d-column items do not fit %d-column blocks", (int)CW, 1 << bg.bc_shift);
     const int64_t n_cg = (pl->n_cliques + Q - 1) / Q;
     const int64_t n_chunks = (p + CW - 1) / CW;
     const int64_t n_items = n_cg * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique group, chunk) items for one grid");
-    const int cpb = bg.bc_shift >= 62 ? 62 : bg.bc_shift - 6;
+    const int cpb = bg.bc_shift >= 62 ? 62 : bg.bc_shift - CW_SHIFT;
     // 32-bit row offsets when every block (column-blocked slabs) spans < 4 GiB
     const bool off32 = bg.bc_shift < 62 && bg.bs_x * 4 <= (int64_t)0xffffffffLL &&
                        bg.bs_y * 4 <= (int64_t)0xffffffffLL;
-#define NIIDMIX_CQ(O) if (late) NIIDMIX_CQL(O, true); else NIIDMIX_CQL(O, false)
-#define NIIDMIX_CQL(O, L) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O, L>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
-    // NIIDMIX_CLIQUE_QLATE=1: gateway gathers after the group sums (A/B)
-    const char *le = getenv("NIIDMIX_CLIQUE_QLATE");
-    const bool late = le && atoi(le) == 1;
-    if (off32) { NIIDMIX_CQ(true); } else { NIIDMIX_CQ(false); }
+#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
+    if (off32) NIIDMIX_CQ(true); else NIIDMIX_CQ(false);
 #undef NIIDMIX_CQ
-#undef NIIDMIX_CQL
     return check_launch("k_mix_clique_q");
 }
 
-template <int W, int R, int OCC, int GA>
+template <int W, int R, int OCC, int GA, int Q = 4>
 int launch_clique_q_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                       const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
     switch (pl->n_groups) {
-        case 1: return launch_clique_q<1, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 2: return launch_clique_q<2, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 3: return launch_clique_q<3, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 4: return launch_clique_q<4, W, R, OCC, GA>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 1: return launch_clique_q<1, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 2: return launch_clique_q<2, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 3: return launch_clique_q<3, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 4: return launch_clique_q<4, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
 }
@@ -2463,17 +2441,19 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
     if (!vec4) return set_error(NIIDMIX_EUNSUPPORTED, "clique kernel needs p, ld multiples of 4 and 16-B aligned slabs");
     if (waves == 0 && use_clique_q(pl, bg)) {
         // tile: <waves>x<slots>x<occupancy>x<gateway gathers per batch>; NIIDMIX_CLIQUE_QT overrides
-        int qw = 0, qr = 0, qo = 0, qg = 0;
-        if (const char *e = getenv("NIIDMIX_CLIQUE_QT")) sscanf(e, "%dx%dx%dx%d", &qw, &qr, &qo, &qg);
+        int qw = 0, qr = 0, qo = 0, qg = 0, qq = 4;
+        if (const char *e = getenv("NIIDMIX_CLIQUE_QT")) sscanf(e, "%dx%dx%dx%dx%d", &qw, &qr, &qo, &qg, &qq);
         if (qw == 0) {
             if (mc <= 104) { qw = 8; qr = 13; qo = 4; qg = 13; }
             else { qw = 16; qr = 7; qo = 8; qg = 2; }
         }
         if (qw * qr < mc) return set_error(NIIDMIX_EINVAL, "clique tile %dx%d < %d members", qw, qr, mc);
-#define NIIDMIX_QT(W, R, O, GA) if (qw == W && qr == R && qo == O && qg == GA) return launch_clique_q_g<W, R, O, GA>(x, ld_x, y, ld_y, p, pl, s, bg)
-        NIIDMIX_QT(8, 13, 4, 13); NIIDMIX_QT(16, 7, 8, 2); NIIDMIX_QT(16, 7, 8, 3); NIIDMIX_QT(16, 7, 4, 7);
+#define NIIDMIX_QT(W, R, O, GA, QQ) if (qw == W && qr == R && qo == O && qg == GA && qq == QQ) return launch_clique_q_g<W, R, O, GA, QQ>(x, ld_x, y, ld_y, p, pl, s, bg)
+        NIIDMIX_QT(8, 13, 4, 13, 4); NIIDMIX_QT(16, 7, 8, 2, 4); NIIDMIX_QT(16, 7, 8, 3, 4); NIIDMIX_QT(16, 7, 4, 7, 4);
+        // 8 cliques x 32 columns per item (a chunk's rows are N x 128 B)
+        NIIDMIX_QT(16, 7, 4, 7, 8); NIIDMIX_QT(16, 7, 8, 2, 8);
 #undef NIIDMIX_QT
-        return set_error(NIIDMIX_EUNSUPPORTED, "no multi-clique tile %dx%dx%dx%d", qw, qr, qo, qg);
+        return set_error(NIIDMIX_EUNSUPPORTED, "no multi-clique tile %dx%dx%dx%dx%d", qw, qr, qo, qg, qq);
     }
     if (waves * rpw < mc) {
         rw = 64; ob = 2; v = vmax;  // non-temporal member loads: 1.39 vs 1.47 ms (headline, same box)

@@ -587,7 +587,9 @@ class Mixer:
           rows: clique-contiguous (node i at slab row perm[i], cliques in plan order) — a
                 clique's member rows of a column block are then one contiguous stretch
                 (1000-node d-cliques 1.345 vs 1.375 ms, 10 000 nodes 15.8 vs 16.3 ms);
-          columns: blocks of 1024 (register tile; 10 000 nodes: 256) or 32 for big cliques
+          columns: blocks of 1024 (register tile), 64 for many cliques (>= 4096 member rows: the
+                multi-clique tile's chunk of every row contiguous), 256 for > 64 gateway terms, or
+                32 for big cliques
                 (> 256 members, 32-column items: an item is then one contiguous 128 KB stretch;
                 fully-connected 1000 nodes 1.43 vs 1.77 ms).
         perm is None when the rows are already clique-contiguous."""
@@ -600,6 +602,12 @@ class Mixer:
             perm = None
         if self.plan.max_clique > 256:
             bc = 32
+        elif self.plan.max_clique <= 112 and len(self.plan.member_row) >= Q_ROWS_MIN:
+            # many cliques (k_mix_clique_q's 64-column items, 10 000 nodes): 64-column blocks, so a
+            # column chunk of every row is ONE contiguous N x 256 B stretch.  With 256-column
+            # blocks its rows sat 1 KiB apart and mapped onto a quarter of the L2's sets: the
+            # gateway gathers (one per member) missed the XCD's L2 (PMC reads 1.44 x algorithmic)
+            bc = int(os.environ.get("NIIDMIX_Q_BLOCK_COLS", "64"))
         else:
             bc = 256 if self.plan.max_clique_res > 64 else memory_block_cols()
         return perm, bc
@@ -694,6 +702,10 @@ class Mixer:
         else:
             raise ValueError(f"unknown kernel {k!r}")
         return out
+
+
+# member rows from which the launcher picks the multi-clique tile (niidmix.hip kQRowsMin)
+Q_ROWS_MIN = 4096
 
 
 def memory_block_cols():

@@ -2,14 +2,16 @@
 layouts and launch paths as bench.py --config dcliques10000 and the multi-GPU stripes:
 
   * the single-GPU fast round exactly as benched: relabeled (clique-contiguous) rows, column-blocked
-    VMM slabs [4096, 10000, 256] (block width 256: a clique gathers 99 gateway rows, > 64), the
-    clique kernel; blocks 0, 2047 and 4095 against the oracle (block 4095 starts 1.05e10 elements
-    into the slab: past 2^31, 2^32 and 2^33), plus column-sum preservation over every block;
+    VMM slabs [16384, 10000, 64] (the multi-clique tile's layout: a 64-column chunk of every row is
+    one contiguous stretch), the clique kernel (k_mix_clique_q); the first, middle and last blocks
+    against the oracle (the last starts 1.05e10 elements into the slab: past 2^31, 2^32 and 2^33),
+    plus column-sum preservation over every block; and the same on the round-2 layout
+    [4096, 10000, 256] (NIIDMIX_Q_BLOCK_COLS=256);
   * the exact default (tile-lds-exact, 199 staged rows per clique -> 96-column items) on row-major
     [10000, 2^20] slabs, bitwise on windows that straddle item boundaries, the ragged last item and
     rows whose offsets exceed 2^33 elements;
   * one rank of the 8000-node weak N=8 column-stripe shape (StripedMixer: 79 gateway terms per
-    clique, B = 256), windows against the oracle and column sums over the whole stripe.
+    clique, B = 64), windows against the oracle and column sums over the whole stripe.
 
 Columns of Θ' = Wᵀ Θ are independent (d_sgd.py:96-116 mixes every tensor element-wise), so a column
 window of the oracle is the full computation restricted to those columns.  Reference topology:
@@ -52,23 +54,27 @@ def _blocked_colsum_gap(xb, yb):
     return gap
 
 
-def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod):
+@pytest.mark.parametrize("bc_env", ["", "256"])
+def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod, monkeypatch, bc_env):
     from niidmix import memory, ops
+    if bc_env:
+        monkeypatch.setenv("NIIDMIX_Q_BLOCK_COLS", bc_env)
     csr, cliques = dc10k
     m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
     assert m.kernel_for("fast") == "clique" and m.plan.max_clique_res == 99
     perm, bc = m.device_layout()
-    assert perm is not None and bc == 256
+    assert perm is not None and bc == (int(bc_env) if bc_env else 64)
     m = m.relabeled(perm)
     xb = memory.empty_blocked(10000, P_FULL, gpu, bc)
-    assert tuple(xb.shape) == (4096, 10000, 256)
+    kb = P_FULL // bc
+    assert tuple(xb.shape) == (kb, 10000, bc)
     xb.normal_(generator=torch.Generator(device=gpu).manual_seed(10))
     yb = memory.empty_blocked(10000, P_FULL, gpu, bc)
     yb.fill_(float("nan"))                       # every output element must be written
     m.mix_blocked(xb, yb, P_FULL)
     torch.cuda.synchronize()
-    assert 4095 * xb.stride(0) > (1 << 33)
-    for k in (0, 2047, 4095):
+    assert (kb - 1) * xb.stride(0) > (1 << 33)
+    for k in (0, kb // 2 - 1, kb - 1):
         _check_fast(oracle_mod, m.csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
     assert not torch.isnan(yb).any().item()
     assert _blocked_colsum_gap(xb, yb) < 2e-3
@@ -108,12 +114,12 @@ def test_dcliques10000_tile_lds_exact_rowmajor(dc10k, gpu, oracle_mod):
 
 
 def test_dcliques8000_stripe_rank7(gpu, oracle_mod):
-    """Weak-scaling N=8's per-rank shape: 8000 nodes (80 cliques, 79 gateway terms each, B = 256),
+    """Weak-scaling N=8's per-rank shape: 8000 nodes (80 cliques, 79 gateway terms each, B = 64),
     rank 7's column stripe [917504, 1048576) of P = 2^20 through StripedMixer."""
     from niidmix.shard import StripedMixer
     sm = StripedMixer.dcliques(8000, 100, world=8, rank=7, interclique="fully-connected",
                                device=gpu, p=P_FULL)
-    assert sm.blocked and sm.block_cols == 256 and sm.mixer.plan.max_clique_res == 79
+    assert sm.blocked and sm.block_cols == 64 and sm.mixer.plan.max_clique_res == 79
     assert (sm.c0, sm.c1) == (7 * (P_FULL // 8), P_FULL)
     x = torch.randn(8000, sm.p_local, device=gpu, generator=torch.Generator(device=gpu).manual_seed(12))
     xb, yb = sm.to_layout(x), sm.empty()

@@ -484,7 +484,7 @@ def test_bigclique_blocked_layout(n, size, inter, gpu):
         m.mix_blocked(xo, oo, p)
 
 
-@pytest.mark.parametrize("tile", ["8x13x4x13", "16x7x8x2", "16x7x4x7"])
+@pytest.mark.parametrize("tile", ["8x13x4x13", "16x7x8x2", "16x7x4x7", "16x7x4x7x8", "16x7x8x2x8"])
 @pytest.mark.parametrize("name", golden_cases())
 def test_multi_clique_tile_vs_golden(name, tile, gpu, oracle_mod, monkeypatch):
     """The multi-clique tile (k_mix_clique_q: 4 cliques x 64 columns per item, the default for
