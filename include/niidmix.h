@@ -105,9 +105,11 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 /* The same round over an ELL layout of the same W^T rows, for low-degree graphs (ring, grid,
  * random regular): row r's entries are ell_col / ell_val[r*k .. r*k + ell_len[r]) in the CSR's
  * order (self first), padded to k entries (the padding is never read as a term).  k: 3, 5 or 8.
- * The gathers depend on one descriptor load (no row_ptr step) and a wave streams several column
- * chunks of its row.  mode as niidmix_mix_csr_f32 (EXACT / FAST, | NIIDMIX_FLAG_AVERAGE_ONLY);
- * bit-identical to it in EXACT mode. */
+ *   x  [>= max(n_rows, max(col)+1), ld_x]: row r's own data (its first entry, normally r itself) is
+ *      loaded before its descriptors arrive, so x must hold at least n_rows rows
+ * The descriptors are scalar loads (one row per wave) and a wave streams several column chunks of
+ * its row.  mode as niidmix_mix_csr_f32 (EXACT / FAST, | NIIDMIX_FLAG_AVERAGE_ONLY); bit-identical
+ * to it in EXACT mode. */
 int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                         int64_t p, int k, const int32_t *ell_col, const float *ell_val,
                         const int32_t *ell_len, int mode, void *stream);

@@ -292,11 +292,6 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
     const int64_t row = (local % n_row_groups) * 4 + wave;
     const int64_t c_beg = slice * CH * CW;
     if (row >= n_rows || c_beg >= p) return;  // wave-uniform
-    const int li = lane < K ? lane : K - 1;
-    const int d_col = ell_col[row * K + li];
-    const float d_val = ell_val[row * K + li];
-    const int len = __builtin_amdgcn_readfirstlane(ell_len[row]);
-    // gathers of every chunk of the slice, all in flight before the first use
     float xv[CH][K][NE];
     int64_t cs[CH][S];
     bool ok[CH][S];
@@ -308,9 +303,35 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
             ok[c][q] = cq < p;                // p % VW == 0: a slot is all-in or all-out
             cs[c][q] = ok[c][q] ? cq : 0;
         }
+    // the row's own data first (self is its list's first entry, d_sgd.py:105): its loads need no
+    // descriptor, so they are in flight while the descriptors arrive
+    {
+        const float *src = x + row * ld_x;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int q = 0; q < S; ++q) ldv<VW>(src + cs[c][q], xv[c][0] + q * VW);
+    }
+    // descriptors by scalar loads (the row is wave-uniform): (col, val) of entry j
+    const int64_t e0 = row * K;
+    const int len = ell_len[row];
+    int colj[K];
+    float valj[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const float *src = x + (int64_t)__builtin_amdgcn_readlane(d_col, j < len ? j : 0) * ld_x;
+        colj[j] = ell_col[e0 + j];
+        valj[j] = ell_val[e0 + j];
+    }
+    if (colj[0] != (int)row) {                // wave-uniform; not the plugin's layout: reload
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int q = 0; q < S; ++q) ldv<VW>(x + (int64_t)colj[0] * ld_x + cs[c][q], xv[c][0] + q * VW);
+    }
+    // gathers of every chunk of the slice, all in flight before the first use
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+        const float *src = x + (int64_t)colj[j < len ? j : 0] * ld_x;
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -325,7 +346,7 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 #pragma unroll
         for (int j = 0; j < K; ++j)
             if (j < len) {                                                            // wave-uniform
-                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_val), j));
+                const float w = valj[j];
 #pragma unroll
                 for (int e = 0; e < NE; ++e) acc[e] = axpy<EXACT>(w, xv[c][j][e], acc[e]);
             }
@@ -1608,7 +1629,30 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // the remaining rows), s43 dz, s44 weight, s46 skipped row * 2 / row index, s47 position.  VGPR
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
 // saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
-#define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
+// updates of the first NR = 4, 8, 12 or 16 accumulator pairs (a tile of <= NR rows keeps them in
+// v[32 : 32 + 2 NR); a 100-member clique's full-height tiles are 16 x 6 + 4 rows)
+#define NIIDMIX_PKADD4(T, A, B, C, D)                                                               \
+    "v_pk_add_f32 v[" A "], v[" A "], " T "\n\tv_pk_add_f32 v[" B "], v[" B "], " T "\n\t"          \
+    "v_pk_add_f32 v[" C "], v[" C "], " T "\n\tv_pk_add_f32 v[" D "], v[" D "], " T "\n\t"
+#define NIIDMIX_ADDQ0(T) NIIDMIX_PKADD4(T, "32:33", "34:35", "36:37", "38:39")
+#define NIIDMIX_ADDQ1(T) NIIDMIX_PKADD4(T, "40:41", "42:43", "44:45", "46:47")
+#define NIIDMIX_ADDQ2(T) NIIDMIX_PKADD4(T, "48:49", "50:51", "52:53", "54:55")
+#define NIIDMIX_ADDQ3(T) NIIDMIX_PKADD4(T, "56:57", "58:59", "60:61", "62:63")
+#define NIIDMIX_FMAQ(XD, A, B, C, D)                                                                \
+    NIIDMIX_FMA1("v[" A "]", XD) NIIDMIX_FMA1("v[" B "]", XD) NIIDMIX_FMA1("v[" C "]", XD)            \
+    NIIDMIX_FMA1("v[" D "]", XD)
+#define NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ(XD, "32:33", "34:35", "36:37", "38:39")
+#define NIIDMIX_FMAQ1(XD) NIIDMIX_FMAQ(XD, "40:41", "42:43", "44:45", "46:47")
+#define NIIDMIX_FMAQ2(XD) NIIDMIX_FMAQ(XD, "48:49", "50:51", "52:53", "54:55")
+#define NIIDMIX_FMAQ3(XD) NIIDMIX_FMAQ(XD, "56:57", "58:59", "60:61", "62:63")
+#define NIIDMIX_SEG_MUL(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t"
+#define NIIDMIX_SEG_UPD_EXACT(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADD16("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT12(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]") NIIDMIX_ADDQ1("%[pr]") NIIDMIX_ADDQ2("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT8(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]") NIIDMIX_ADDQ1("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT4(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]")
+#define NIIDMIX_UPD_FAST12(XD) NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ1(XD) NIIDMIX_FMAQ2(XD)
+#define NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ1(XD)
+#define NIIDMIX_UPD_FAST4(XD) NIIDMIX_FMAQ0(XD)
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
     "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
@@ -1706,14 +1750,22 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                    [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB)             \
                  : "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "m0", "scc", \
                    "memory")
-template <bool EXACT, int RB>
+// NR: the tile's rows sit in accumulator pairs 0 .. NR-1 (4, 8, 12 or 16); runs update only those
+template <bool EXACT, int RB, int NR>
 __device__ __forceinline__ void tlds16_walk(Acc16 &acc, int dx, int dy, int dz, int cnt, int base,
                                             int w0, int w1, int lane8) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
+    static_assert(NR == 4 || NR == 8 || NR == 12 || NR == 16, "rows in multiples of 4");
     uint64_t x0, x1, x2, x3, pr;
     uint32_t sv0, sv1, q0, q1, va;
-    if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
-    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
+    if constexpr (EXACT && NR == 16) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
+    else if constexpr (EXACT && NR == 12) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT12, NIIDMIX_MSK_EXACT);
+    else if constexpr (EXACT && NR == 8) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT8, NIIDMIX_MSK_EXACT);
+    else if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT4, NIIDMIX_MSK_EXACT);
+    else if constexpr (NR == 16) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
+    else if constexpr (NR == 12) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST12, NIIDMIX_MSK_FAST);
+    else if constexpr (NR == 8) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST8, NIIDMIX_MSK_FAST);
+    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST4, NIIDMIX_MSK_FAST);
     (void)pr;
 }
 
@@ -1894,6 +1946,9 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && (NIIDMIX_TLDS_SPLIT == 0 || NIIDMIX_TLDS_SPLIT == 2)) {
             {                                                            // segment loop (tile.py)
                 const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
+                // rows of the tile: pairs 0 .. nr-1 (niidmix.tile fills a tile's slots from the top;
+                // unused slots have row -1 and are never skipped or masked)
+                const int nr = 32 - __builtin_clz((uint32_t)__ballot(lane < RT && d_row >= 0) | 1u);
                 const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
                 for (int sb = sb0; sb < sb1; sb += 64) {
                     // 64 segments' descriptors lane-parallel (one int4 each), handed out by
@@ -1902,8 +1957,11 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     // y = the rows that take it, z = its weight (fp32 bits)
                     const int cnt = sb1 - sb < 64 ? sb1 - sb : 64;
                     const int4 da = reinterpret_cast<const int4 *>(seg)[sb + (lane < cnt ? lane : cnt - 1)];
-                    tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base,
-                                                             w0, w1, lane8);
+                    constexpr int RB = rs * (int)sizeof(f2);
+                    if (nr <= 4) tlds16_walk<EXACT, RB, 4>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
+                    else if (nr <= 8) tlds16_walk<EXACT, RB, 8>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
+                    else if (nr <= 12) tlds16_walk<EXACT, RB, 12>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
+                    else tlds16_walk<EXACT, RB, 16>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
                 }
                 goto tile_epilogue;
             }

@@ -526,7 +526,8 @@ class Mixer:
         # rows fit the LDS stage); NIIDMIX_TILE_LDS_RT=8|16|32 picks the tile height
         csr, dev = self.csr, self.device
         self.tlds, self.tlds_reason = (None, "average degree < 8")
-        if csr.nnz >= 9 * max(csr.n, 1):
+        # NIIDMIX_TLDS_ANY_DEGREE=1 builds them for low-degree graphs too (ring / grid probes)
+        if csr.nnz >= 9 * max(csr.n, 1) or os.environ.get("NIIDMIX_TLDS_ANY_DEGREE") == "1":
             rt = int(os.environ.get("NIIDMIX_TILE_LDS_RT", "16"))
             grp = self.cliques
             if not grp:

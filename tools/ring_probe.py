@@ -64,6 +64,22 @@ def main():
                     else:
                         m(y, out=x, kernel=kern)
             t_graph[kern + (f"/ch{ch}" if ch else "")] = timed(lambda i: g.replay(), max(1, a.iters // 50)) / 50
+    # the LDS-staged tiles on the ring (groups of consecutive rows, each source row staged once per
+    # group instead of gathered by ~3 waves)
+    os.environ["NIIDMIX_TLDS_ANY_DEGREE"] = "1"
+    m2 = ops.Mixer(csr=csr, cliques=cl, device=dev)
+    assert m2.tlds is not None, m2.tlds_reason
+    for kern in ("tile-lds-fast", "tile-lds-exact"):
+        g = torch.cuda.CUDAGraph()
+        m2(x, out=y, kernel=kern)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            for i in range(50):
+                if i % 2 == 0:
+                    m2(x, out=y, kernel=kern)
+                else:
+                    m2(y, out=x, kernel=kern)
+        t_graph[kern] = timed(lambda i: g.replay(), max(1, a.iters // 50)) / 50
     numel = n * p - (n * p) % 4
     xa, ya = x.view(-1)[:numel], y.view(-1)[:numel]
     cp = _lib.lib.niidmix_stream_copy_f32
