@@ -813,9 +813,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[r][e] = has ? __builtin_fmaf(w, ga[r][e], v[r][e]) : v[r][e];
     }
-    // gathers of slots [NA, RPW) in batches of NA, in ga's registers (gathering them all after the
-    // group sums instead -- so the chunk's other items had loaded their rows into L2 first --
-    // measured slower: 18.1 vs 15.5 ms at 10 000 nodes, with register spills)
+    // gathers of slots [NA, RPW) in batches of NA, in ga's registers.  Issuing gateway gathers
+    // later, so that the chunk's other items have their rows in L2 first, measured slower at 10 000
+    // nodes every way tried: all after the group sums 18.1 vs 15.5 ms; the first batch after this
+    // wave's member rows arrived 18.9 / 27.6 ms (13 gathers per batch, spills) and 15.2 ms (7)
+    // against 14.3 ms (profiles/r03/clique_q_late_gathers_10k.txt)
 #pragma unroll
     for (int b0 = NA; b0 < RPW; b0 += NA) {
 #pragma unroll
