@@ -249,13 +249,21 @@ typedef struct niidmix_tile_lds_plan {
     const int32_t *grp_src_rows;
     /* optional (rt 16; NULL = the per-position loop): the positions cut into segments, runs read
      * from consecutive LDS slots with immediate offsets (niidmix.tile.build_tile_segments):
-     *   seg_ptr [n_sub+1] int32 segments of each tile;  seg [n_seg * 8] int32 per segment: first
-     *   slot, length (| 1 << 30: one position for the generic path, word 7 its position index),
-     *   weight-select bits (2 words), skip bits (2 words), first skipped tile row, first position;
-     *   seg_w [n_sub * 2] fp32 the tile's two weights */
+     *   seg_ptr [n_sub+1] int32 segments of each tile;  seg [n_seg * 4] int32 per segment:
+     *   a run: first slot | length << 12 | first skipped tile row << 20, weight-select bits, skip
+     *   bits, 0;  a masked position: slot | 1 << 30, the tile rows that take it, its weight (fp32
+     *   bits), 0;  seg_w [n_sub * 2] fp32 the tile's two weights */
     const int32_t *seg_ptr;
     const int32_t *seg;
     const float *seg_w;
+    /* optional (rt 16 with segments, EXACT mode; NULL = the segment walker): the positions as
+     * matrix-core lists (niidmix.tile.build_tile_mfma_positions), applied by v_mfma_f32_16x16x4_f32
+     * 4 positions at a time, bit-identical; a block whose staged rows hold a non-finite value or
+     * one below 1e-30 in magnitude takes the segment walker instead:
+     *   mf_ptr [n_sub+1] int32 entries of each tile (multiples of 4);  mf [n_mf * 4] int32 per
+     *   entry: slot, weight (fp32 bits), tile rows that take it, 0 */
+    const int32_t *mf_ptr;
+    const int32_t *mf;
 } niidmix_tile_lds_plan;
 
 int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

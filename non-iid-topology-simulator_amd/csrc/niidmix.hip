@@ -1809,6 +1809,14 @@ __device__ __forceinline__ void apply_mask(TileAcc<RT> &acc, uint32_t m, Op op) 
 #ifndef NIIDMIX_TLDS_SPLIT
 #define NIIDMIX_TLDS_SPLIT 0
 #endif
+// The exact matrix-core path in the RT-16 segment kernels (1) or not (0).
+#ifndef NIIDMIX_TLDS_MF
+#define NIIDMIX_TLDS_MF 1
+#endif
+// Matrix-core path time split (tuning builds only): 3 no position loop.  Product builds leave it 0.
+#ifndef NIIDMIX_MF_SPLIT
+#define NIIDMIX_MF_SPLIT 0
+#endif
 // Stage by LDS-DMA (1) or through registers (0; tuning A/B builds only).
 #ifndef NIIDMIX_TLDS_GLDS
 #define NIIDMIX_TLDS_GLDS 1
@@ -1832,7 +1840,8 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
     const int32_t *__restrict__ seg_ptr, const int32_t *__restrict__ seg,
-    const float *__restrict__ seg_w) {
+    const float *__restrict__ seg_w, const int32_t *__restrict__ mf_ptr,
+    const int32_t *__restrict__ mf) {
     // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
     // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
@@ -1923,6 +1932,125 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         }
     }
     __syncthreads();
+    if constexpr (NIIDMIX_TLDS_MF && EXACT && SEG && RT == 16 && NIIDMIX_TLDS_SPLIT == 0) {
+        // 2'. Matrix-core path (exact): v_mfma_f32_16x16x4_f32 applies 4 positions to the tile's 16
+        // rows x 16 columns at a time as a k-ordered chain of single-rounding fmas: A[col][k] =
+        // fl(w_k * x_k[col]), B[k][row] = 1 if the row takes position k else 0, so a row that
+        // takes k gets fl(acc + fl(w x)) -- bit for bit the reference's add_(w*p) -- and the
+        // others acc + (+-0), which is acc unless acc is -0 or the product is not finite.  Hence
+        // the block-wide check: every staged value finite with |x| >= 1e-30 (each row's
+        // accumulator is then non-zero from its self term on); otherwise the block falls back to
+        // the segment walker below.  Position lists: niidmix.tile.build_tile_mfma_positions.
+        // Lane l holds D[i = 4 (l >> 4) + r][j = l & 15]: tile row j, parameter columns
+        // 8 i + cb (cb: the 8 accumulators), i.e. the 32 consecutive columns 32 (l >> 4) .. +31.
+        if (mf_ptr != nullptr) {
+            bool bad = false;
+            {
+                const int nf = (grp_src_ptr[grp + 1] - grp_src_ptr[grp]) * (int)CW;
+                for (int i = 4 * (int)threadIdx.x; i < nf; i += 4 * (int)blockDim.x) {
+                    const float4 v = *reinterpret_cast<const float4 *>(lds_tile + i);
+                    const float m0 = fminf(fminf(fabsf(v.x), fabsf(v.y)), fminf(fabsf(v.z), fabsf(v.w)));
+                    const float m1 = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+                    // NaN: fminf / fmaxf drop it, so test each value too
+                    bad |= !(m0 >= 1e-30f) || !(m1 <= 3.4028235e38f) ||
+                           (v.x != v.x) || (v.y != v.y) || (v.z != v.z) || (v.w != v.w);
+                }
+            }
+            if (!__syncthreads_or(bad)) {
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                const int jr = lane & 15, g4 = lane >> 4;
+                const int tb = grp_tile_ptr[grp], te = grp_tile_ptr[grp + 1];
+                // a block has at most one tile per wave (64 * max_tiles threads)
+                const int sub = tb + wave;
+                const bool have = sub < te;                                  // wave-uniform
+                const int li = lane < RT ? lane : RT - 1;
+                const int d_row = have ? sub_rows[sub * RT + li] : -1;
+                const int d_slot = have ? sub_slot[sub * RT + li] : 0;
+                const float d_ws = have ? sub_wself[sub * RT + li] : 0.f;
+                const int row_j = __shfl(d_row, jr), slot_j = __shfl(d_slot, jr);
+                const float ws_j = __shfl(d_ws, jr);
+                float *srow = lds_tile + slot_j * (int)CW + 32 * g4;
+                f4v acc[8];
+                if (have) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {                            // self: z + fl(ws * xs)
+                        const float4 a = *reinterpret_cast<const float4 *>(srow + 8 * r);
+                        const float4 b = *reinterpret_cast<const float4 *>(srow + 8 * r + 4);
+                        const float xs[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+                        for (int cb = 0; cb < 8; ++cb) acc[cb][r] = xs[cb] * 0.f + ws_j * xs[cb];
+                    }
+                    const int e0 = mf_ptr[sub], e1 = mf_ptr[sub + 1];
+                    for (int eb = e0; eb < e1; eb += 64) {
+                        const int cnt = e1 - eb < 64 ? e1 - eb : 64;           // a multiple of 4
+                        const int4 d = reinterpret_cast<const int4 *>(mf)[eb + (lane < cnt ? lane : cnt - 1)];
+                        for (int q = 0; q < cnt; q += 4) {
+                            if (NIIDMIX_MF_SPLIT == 3) break;                 // tuning builds only
+                            const int src = q + g4;                           // position q + k, k = l >> 4
+                            const int slot = __shfl(d.x, src);
+                            const float w = __int_as_float(__shfl(d.y, src));
+                            const uint32_t m = (uint32_t)__shfl(d.z, src);
+                            const float bv = ((m >> jr) & 1u) ? 1.f : 0.f;
+                            const float *xr = lds_tile + slot * (int)CW + 8 * jr;
+                            const float4 x0 = *reinterpret_cast<const float4 *>(xr);
+                            const float4 x1 = *reinterpret_cast<const float4 *>(xr + 4);
+                            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.x, bv, acc[0], 0, 0, 0);
+                            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.y, bv, acc[1], 0, 0, 0);
+                            acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.z, bv, acc[2], 0, 0, 0);
+                            acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.w, bv, acc[3], 0, 0, 0);
+                            acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.x, bv, acc[4], 0, 0, 0);
+                            acc[5] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.y, bv, acc[5], 0, 0, 0);
+                            acc[6] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.z, bv, acc[6], 0, 0, 0);
+                            acc[7] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.w, bv, acc[7], 0, 0, 0);
+                        }
+                    }
+                    // update_models: o = z + acc (z from the row's own staged value), in place
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float4 a = *reinterpret_cast<const float4 *>(srow + 8 * r);
+                        const float4 b = *reinterpret_cast<const float4 *>(srow + 8 * r + 4);
+                        const float xs[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+                        for (int cb = 0; cb < 8; ++cb)
+                            if (!avg_only) acc[cb][r] = xs[cb] * 0.f + acc[cb][r];
+                    }
+                }
+                // Stores: a lane holds 32 consecutive columns of ONE row, so storing from here would
+                // write 64 rows' 8-16 B pieces per instruction (measured 25 ms per round).  Once every
+                // wave is done reading the stage, each row's result goes to its own staged row
+                // (distinct slots: a group's rows are distinct), then is stored row by row with the
+                // walker's coalesced pattern (lane = column pair).
+                __syncthreads();
+                if (have && row_j >= 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (32 * g4 + 8 * r < (int)CW) {                     // CW: a multiple of 8
+                            *reinterpret_cast<float4 *>(srow + 8 * r) =
+                                make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
+                            *reinterpret_cast<float4 *>(srow + 8 * r + 4) =
+                                make_float4(acc[4][r], acc[5][r], acc[6][r], acc[7][r]);
+                        }
+                }
+                if (have) {
+                    const int64_t col = c0 + 2 * lane;
+                    const bool okc = lane < rs && col < p;
+                    const int slc = lane < rs ? lane : rs - 1;
+#pragma unroll
+                    for (int r = 0; r < RT; ++r) {
+                        const int row = __builtin_amdgcn_readlane(d_row, r);
+                        if (row < 0) continue;                               // wave-uniform
+                        const f2 o = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + slc];
+                        if (okc) {
+                            float *dst = y + (int64_t)row * ld_y + col;
+                            __builtin_nontemporal_store(o.x, dst);
+                            __builtin_nontemporal_store(o.y, dst + 1);
+                        }
+                    }
+                }
+                return;                                                      // block-uniform
+            }
+        }
+    }
     const int64_t col = c0 + 2 * lane;
     const bool ok = lane < rs && col < p;        // p even: a lane's pair is all-in or all-out
     // LDS column index of this lane: lanes >= rs (120- / 96-column items) compute nothing that is
@@ -2978,6 +3106,9 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     // segment loop (RT 16, plan->seg_ptr set): two spare staged rows for its reads past a segment
     const bool seg = plan->rt == 16 && plan->seg_ptr != nullptr;
     if (seg && (!plan->seg || !plan->seg_w)) return set_error(NIIDMIX_EINVAL, "null segment arrays");
+    // matrix-core path (exact mode, segment plans only: the walker is its per-block fallback)
+    const bool mf = seg && mode == NIIDMIX_MODE_EXACT && plan->mf_ptr != nullptr;
+    if (mf && !plan->mf) return set_error(NIIDMIX_EINVAL, "null MFMA position list");
     const int stage_rows = plan->max_src + (seg ? 2 : 0);
     if (plan->rt == 16) {
         auto blocks = [&](int c) {
@@ -3003,7 +3134,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
                        : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, false> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, false> : k_mix_tile_lds<E, R, V, 64, false>); \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)

@@ -28,7 +28,8 @@ import torch
 
 from . import _lib
 from .factor import build_clique_plan
-from .tile import LDS_MAX_WAVES, build_tile_lds_plan, build_tile_plan, build_tile_segments
+from .tile import (LDS_MAX_WAVES, build_tile_lds_plan, build_tile_mfma_positions, build_tile_plan,
+                   build_tile_segments)
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -251,9 +252,12 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                  pos_mask: torch.Tensor, pos_w: torch.Tensor, grp_tile_ptr: torch.Tensor,
                  grp_src_ptr: torch.Tensor, grp_src_rows: torch.Tensor, out: torch.Tensor, rt: int,
                  max_src: int, max_tiles: int, mode: int, seg_ptr: Optional[torch.Tensor] = None,
-                 seg: Optional[torch.Tensor] = None, seg_w: Optional[torch.Tensor] = None) -> None:
+                 seg: Optional[torch.Tensor] = None, seg_w: Optional[torch.Tensor] = None,
+                 mf_ptr: Optional[torch.Tensor] = None, mf: Optional[torch.Tensor] = None) -> None:
     """seg_ptr / seg / seg_w: the plan's segments (niidmix.tile.build_tile_segments, RT 16 only):
-    the kernel's segment loop instead of the per-position loop; bit-identical results."""
+    the kernel's segment loop instead of the per-position loop; bit-identical results.
+    mf_ptr / mf: its MFMA position lists (niidmix.tile.build_tile_mfma_positions; needs the
+    segments, exact mode): the matrix-core path, bit-identical, the walker its per-block fallback."""
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -278,13 +282,20 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
         _req(seg.numel() % 4 == 0 and seg.data_ptr() % 16 == 0, "seg: [S, 4] int32, 16-B aligned")
         _vec("seg_w", seg_w, torch.float32, dev, 2 * t)
         segs = (seg_ptr.data_ptr(), seg.data_ptr(), seg_w.data_ptr())
+    mfs = (None, None)
+    if mf_ptr is not None:
+        _req(seg_ptr is not None and mf is not None, "MFMA position lists: with the segments, mf_ptr and mf")
+        _vec("mf_ptr", mf_ptr, torch.int32, dev, t + 1)
+        _vec("mf", mf, torch.int32, dev)
+        _req(mf.numel() % 4 == 0 and mf.data_ptr() % 16 == 0, "mf: [E, 4] int32, 16-B aligned")
+        mfs = (mf_ptr.data_ptr(), mf.data_ptr() if mf.numel() else mf_ptr.data_ptr())
     _no_overlap(x, out)
     some = sub_ptr.data_ptr()
     plan = _lib.TileLdsPlanC(t, int(rt), g, int(max_src), int(max_tiles), sub_ptr.data_ptr(),
                              sub_rows.data_ptr(), sub_slot.data_ptr(), sub_wself.data_ptr(),
                              pos_slot.data_ptr() or some, pos_mask.data_ptr() or some,
                              pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
-                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs)
+                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs, *mfs)
     rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
                                            out.shape[0], x.shape[1], ctypes.byref(plan), int(mode),
                                            _stream(x))
@@ -401,6 +412,7 @@ _LAZY = {
     "l_sub_slot": "tlds", "l_sub_wself": "tlds", "l_pos_slot": "tlds", "l_pos_mask": "tlds",
     "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
     "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
+    "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds",
     "w_dense": "dense",
     "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell",
 }
@@ -452,6 +464,9 @@ class Mixer:
                       and self.n >= 64)
         self._host = {}           # host-side plans, shared with the Mixers .to() makes
         self.use_segments = True  # RT-16 LDS tiles: segment loop where segments built
+        # exact RT-16 LDS tiles: the matrix-core path (bit-identical, but 4.3 vs 3.2 ms on the
+        # headline: DESIGN §3) only on request, NIIDMIX_TLDS_MFMA=1
+        self.use_mfma = os.environ.get("NIIDMIX_TLDS_MFMA", "0") == "1"
 
     def to(self, device):
         """The same operator on another device, sharing the host-side plans (built once)."""
@@ -540,16 +555,20 @@ class Mixer:
         lp = self.tlds
         # segment loop (RT 16): runs of consecutive LDS slots read at immediate offsets
         # (niidmix.tile.build_tile_segments); NIIDMIX_TLDS_SEG=0 keeps the per-position loop
-        ts = None
+        ts = tm = None
         if lp.tile.rt == 16 and os.environ.get("NIIDMIX_TLDS_SEG", "1") != "0":
             ts = self._hosted(("tseg", lp.tile.rt), lambda: build_tile_segments(lp))
+            # position lists of the matrix-core exact path (used when Mixer.use_mfma)
+            if ts is not None:
+                tm = self._hosted(("tmf", lp.tile.rt), lambda: build_tile_mfma_positions(lp))
         # unbound: `self` may be the lazy builder's scratch object, whose attribute lookups (bound
         # methods included) fall through to the Mixer
-        Mixer.set_tile_lds_plan(self, lp, ts)
+        Mixer.set_tile_lds_plan(self, lp, ts, tm)
 
-    def set_tile_lds_plan(self, lp, ts=None):
-        """Upload an LDS tile plan (niidmix.tile.build_tile_lds_plan) and its segments (or None:
-        the per-position loop) to this Mixer's device."""
+    def set_tile_lds_plan(self, lp, ts=None, tm=None):
+        """Upload an LDS tile plan (niidmix.tile.build_tile_lds_plan), its segments (or None: the
+        per-position loop) and its MFMA position lists (or None: the segment walker) to this
+        Mixer's device."""
         dev = self.device
         tp = lp.tile
         self.tlds = lp
@@ -569,6 +588,10 @@ class Mixer:
             self.s_seg_ptr = torch.from_numpy(ts.seg_ptr).to(dev)
             self.s_seg = torch.from_numpy(np.ascontiguousarray(ts.seg).reshape(-1)).to(dev)
             self.s_seg_w = torch.from_numpy(np.ascontiguousarray(ts.seg_w).reshape(-1)).to(dev)
+        self.tmf = tm if ts is not None else None
+        if self.tmf is not None:
+            self.m_mf_ptr = torch.from_numpy(tm.mf_ptr).to(dev)
+            self.m_mf = torch.from_numpy(np.ascontiguousarray(tm.mf).reshape(-1)).to(dev)
 
     def _build_ell(self):
         lay = self._hosted("ell", lambda: ell_layout(self.csr))
@@ -690,6 +713,9 @@ class Mixer:
             ts = self.tseg
             segs = (self.s_seg_ptr, self.s_seg, self.s_seg_w) if \
                 self.use_segments and ts is not None and ts.lp is lp else ()
+            if segs and k == "tile-lds-exact" and self.use_mfma and self.tmf is not None \
+                    and self.tmf.lp is lp:
+                segs = segs + (self.m_mf_ptr, self.m_mf)
             mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
                          self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
                          self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,

@@ -507,3 +507,93 @@ def segments_row_lists(lp, ts):
         for r, lst in lists.items():
             out[int(rows[r])] = lst
     return out
+
+
+@dataclass
+class TileMfmaPositions:
+    """The positions of an RT-16 LDS tile plan as MFMA position lists (k_mix_tile_lds's matrix-core
+    path, exact mode; include/niidmix.h niidmix_tile_lds_plan.mf*).
+
+    v_mfma_f32_16x16x4_f32 is bit for bit a k-ordered chain of fp32 fmas, one rounding each
+    (tools/mfma_exact_probe.hip: 0 mismatches in 2.7e8 chained outputs).  With A[col][k] =
+    fl(w_k * x_{slot k}[col]) and B[k][row] = 1 when the tile row takes position k, else 0, each step
+    is fl(acc + fl(w x)) for the rows that take it -- the reference's add_(w*p) -- and acc + (+-0)
+    for the others, which leaves acc unchanged unless acc is -0 (the kernel's per-block check makes
+    sure it never is: every staged value is finite and at least 1e-30 in magnitude, so each row's
+    accumulator is non-zero after its self term; else the block takes the segment walker).
+    A position whose rows carry different weights becomes one entry per weight class (each row
+    still takes it once, at this point of its own order).  Tiles are padded to a multiple of 4
+    entries with (slot 0, weight 0, no rows).
+      mf_ptr [T+1] int32: entries of tile t;  mf [E, 4] int32: slot, weight (fp32 bits), row mask, 0"""
+    mf_ptr: np.ndarray
+    mf: np.ndarray
+    lp: object = None
+
+    @property
+    def n_entries(self):
+        return len(self.mf)
+
+
+def build_tile_mfma_positions(lp):
+    """TileMfmaPositions of a TileLdsPlan (RT 16 tiles)."""
+    tp = lp.tile
+    rt = tp.rt
+    if rt != 16:
+        return None
+    slots = (lp.pos_slot & (POS_UNIFORM - 1)).astype(np.int64)
+    uni = (lp.pos_slot & POS_UNIFORM) != 0
+    ptr, ent = [0], []
+    for t in range(tp.n_sub):
+        real = 0
+        for r in range(rt):
+            if tp.sub_rows[t * rt + r] >= 0:
+                real |= 1 << r
+        n0 = len(ent)
+        for k in range(int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])):
+            m = int(tp.pos_mask[k]) & real
+            if m == 0:
+                continue
+            wr = tp.pos_w[k * rt:(k + 1) * rt]
+            if uni[k]:
+                ent.append((int(slots[k]), int(np.float32(wr[0]).view(np.uint32)), m))
+                continue
+            classes = {}
+            for r in range(rt):
+                if (m >> r) & 1:
+                    wb = int(np.float32(wr[r]).view(np.uint32))
+                    classes[wb] = classes.get(wb, 0) | (1 << r)
+            for wb, cm in classes.items():
+                ent.append((int(slots[k]), wb, cm))
+        while (len(ent) - n0) % 4:
+            ent.append((0, 0, 0))
+        ptr.append(len(ent))
+    arr = np.zeros((len(ent), 4), np.int64)
+    if ent:
+        arr[:, :3] = np.asarray(ent, np.int64)
+    arr = (arr & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    return TileMfmaPositions(mf_ptr=np.asarray(ptr, np.int32), mf=arr.reshape(-1, 4), lp=lp)
+
+
+def mfma_row_lists(lp, tm):
+    """{row: [(src, w), ...]} as the MFMA path applies them (self first) -- for checks."""
+    tp = lp.tile
+    rt = tp.rt
+    gtp = lp.grp_tile_ptr
+    grp_of = np.zeros(tp.n_sub, np.int64)
+    for gi in range(len(gtp) - 1):
+        grp_of[gtp[gi]:gtp[gi + 1]] = gi
+    out = {}
+    mf = tm.mf.view(np.uint32).astype(np.int64)
+    for t in range(tp.n_sub):
+        base = int(lp.grp_src_ptr[grp_of[t]])
+        rows = tp.sub_rows[t * rt:(t + 1) * rt]
+        lists = {r: [(int(rows[r]), np.float32(tp.sub_wself[t * rt + r]))]
+                 for r in range(rt) if rows[r] >= 0}
+        for e in mf[tm.mf_ptr[t]:tm.mf_ptr[t + 1]]:
+            slot, wb, m = int(e[0]), np.uint32(e[1]).view(np.float32), int(e[2])
+            for r in lists:
+                if (m >> r) & 1:
+                    lists[r].append((int(lp.grp_src_rows[base + slot]), np.float32(wb)))
+        for r, lst in lists.items():
+            out[int(rows[r])] = lst
+    return out

@@ -84,7 +84,7 @@ def test_argument_errors_without_gpu():
     assert L.niidmix_mix_tile_f32(16, 4, 16, 4, 1, 4, ctypes.byref(tp), 0, None) == _lib.EALIAS
     # ABI 3: partial overlaps are caught over the full [n_rows, ld] extents (4 rows of ld 8)
     assert L.niidmix_mix_tile_f32(base, 8, base + 4 * 20, 8, 4, 8, ctypes.byref(tp), 0, None) == _lib.EALIAS
-    lp = _lib.TileLdsPlanC(1, 16, 1, 8, 1, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)
+    lp = _lib.TileLdsPlanC(1, 16, 1, 8, 1, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8)   # seg*/mf* NULL
     assert L.niidmix_mix_tile_lds_f32(base, 8, base + 4 * 20, 8, 4, 8, ctypes.byref(lp), 0, None) == _lib.EALIAS
     G = L.niidmix_grad_segment_mean_f32
     assert G(None, 4, 16, 4, 1, 4, 1, 8, 8, None) == _lib.EINVAL

@@ -110,7 +110,8 @@ def _tile_lds_mixer(g, dev, rt):
     lp, why = tile.build_tile_lds_plan(m.csr, cl, rt)
     if lp is None:
         pytest.skip(why)
-    m.set_tile_lds_plan(lp, tile.build_tile_segments(lp) if rt == 16 else None)
+    ts = tile.build_tile_segments(lp) if rt == 16 else None
+    m.set_tile_lds_plan(lp, ts, tile.build_tile_mfma_positions(lp) if ts is not None else None)
     return m
 
 
@@ -202,6 +203,48 @@ def test_tile_lds_segment_loop_bitwise(name, gpu, oracle_mod):
         bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
         ok, worst = oracle_mod.check_tolerance(yf, g["y"], bound, rtol=RTOL)
         assert ok, (name, worst)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_tile_lds_mfma_bitwise(name, gpu, oracle_mod):
+    """The exact matrix-core path (v_mfma_f32_16x16x4_f32 with 0/1 row masks; blocks whose staged
+    rows hold a non-finite or tiny value fall back to the segment walker; Mixer.use_mfma, off by
+    default) is bit-identical to the reference on every golden case, non-finite fixtures included,
+    and to the walker."""
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    m = _tile_lds_mixer(g, gpu, 16)
+    assert m.tmf is not None and m.tmf.lp is m.tlds
+    x = torch.from_numpy(g["x"]).to(gpu)
+    for use in (True, False):
+        m.use_mfma = use
+        y = m(x, kernel="tile-lds-exact").cpu().numpy()
+        assert oracle_mod.bitwise_equal(y, g["y"]), (name, use)
+
+
+@pytest.mark.parametrize("p", [1002, 1 << 16])
+def test_tile_lds_mfma_random_and_fallback_blocks(p, gpu, oracle_mod):
+    """1000-node d-cliques on random data: every block on the matrix cores; then zeros, -0.0, a
+    subnormal, an inf and a NaN planted in a few column chunks, whose blocks take the walker while
+    the rest stay on the MFMA path: bitwise the C oracle either way (ragged last item at p=1002)."""
+    g = load_golden("dcliques1000_fc_p64")
+    m = _tile_lds_mixer(g, gpu, 16)
+    m.use_mfma = True
+    rng = np.random.default_rng(p)
+    x = (rng.standard_normal((1000, p)) * np.exp2(rng.integers(-20, 20, (1000, p)))).astype(np.float32)
+    ref = oracle_mod.mix_exact_c(x, g["row_ptr"], g["col"], g["val"])
+    y = m(torch.from_numpy(x).to(gpu), kernel="tile-lds-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, ref)
+    x2 = x.copy()
+    x2[3, 5] = 0.0
+    x2[17, 130] = -0.0
+    x2[400, 261] = np.float32(1e-42)
+    x2[999, p - 1] = np.inf
+    x2[250, p // 2] = np.nan
+    ref2 = oracle_mod.mix_exact_c(x2, g["row_ptr"], g["col"], g["val"])
+    y2 = m(torch.from_numpy(x2).to(gpu), kernel="tile-lds-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y2, ref2)
 
 
 @pytest.mark.parametrize("n,size,inter", [(1000, 10, "fully-connected"), (600, 30, "smallworld"),

@@ -151,3 +151,66 @@ def test_lds_plan_runs_dcliques():
         pairs += len(slots) - 1
     assert every_row / groups > 0.7, every_row / groups
     assert consecutive / pairs > 0.8, consecutive / pairs
+
+
+def _lds16(g, csr):
+    from niidmix import tile
+    cl = g.get("cliques")
+    if not cl:
+        span = 16 * tile.LDS_MAX_WAVES[16]
+        cl = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
+    lp, why = tile.build_tile_lds_plan(csr, cl, 16)
+    return lp, why
+
+
+def _assert_rows_are_csr(rows, csr):
+    assert sorted(rows) == list(range(csr.n))
+    for i in range(csr.n):
+        b, e = csr.row_ptr[i], csr.row_ptr[i + 1]
+        want = [(int(c), float(np.float32(w))) for c, w in zip(csr.col[b:e], csr.val[b:e])]
+        assert [(int(c), float(w)) for c, w in rows[i]] == want, i
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_segments_apply_csr_rows(name):
+    """The segment walker's view of an RT-16 LDS plan (runs + masked entries) gives every row
+    exactly its CSR row, in order (k_mix_tile_lds's segment loop, niidmix.tile.build_tile_segments)."""
+    from niidmix import tile
+    g = load_golden(name)
+    csr = _csr(g)
+    lp, why = _lds16(g, csr)
+    if lp is None:
+        pytest.skip(why)
+    ts = tile.build_tile_segments(lp)
+    assert ts is not None and ts.seg.shape[1] == tile.SEG_WORDS
+    _assert_rows_are_csr(tile.segments_row_lists(lp, ts), csr)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_mfma_positions_apply_csr_rows(name):
+    """The MFMA path's position lists (one entry per weight class, 4-entry groups) give every row
+    exactly its CSR row, in order; padding entries take no row."""
+    from niidmix import tile
+    g = load_golden(name)
+    csr = _csr(g)
+    lp, why = _lds16(g, csr)
+    if lp is None:
+        pytest.skip(why)
+    tm = tile.build_tile_mfma_positions(lp)
+    assert tm is not None
+    assert np.all(np.diff(tm.mf_ptr) % 4 == 0)
+    assert np.all(tm.mf[:, 2].view(np.uint32) < (1 << 16))
+    _assert_rows_are_csr(tile.mfma_row_lists(lp, tm), csr)
+
+
+def test_mfma_positions_dcliques_headline_shape():
+    """1000-node d-cliques (the headline): ~100 positions per 16-row tile, so the MFMA path issues
+    ~26 groups of 4 positions per tile."""
+    from niidmix import tile
+    from niidmix.generate import dcliques_csr
+    csr, cl = dcliques_csr(1000, 100, "fully-connected", 1337)
+    lp, _ = tile.build_tile_lds_plan(csr, cl, 16)
+    tm = tile.build_tile_mfma_positions(lp)
+    per_tile = np.diff(tm.mf_ptr)
+    assert per_tile.max() <= 112 and per_tile.mean() < 106
+    _assert_rows_are_csr(tile.mfma_row_lists(lp, tm), csr)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Exact-mode (bit-identical) round A/B on the headline topology (tuning tool, not the bench): the
-LDS-staged merged-order tile kernel at tile heights --rts (RT 16: segment loop "seg" and per-position
-loop "pos"), interleaved in one process; results of
+LDS-staged merged-order tile kernel at tile heights --rts (RT 16: matrix-core path "mfma", segment
+walker "seg" and per-position loop "pos"), interleaved in one process; results of
 every variant are checked bitwise against the first (--no-check for the phase-split builds of
 tools/tlds_split.sh, whose results are not the mix).
 
@@ -56,8 +56,9 @@ def main():
     res = {}
     for rep in range(a.reps):
         for rt, m in mixers.items():
-            for meta in (("seg", "pos") if rt == 16 else ("pos",)):
-                m.use_segments = meta == "seg"
+            for meta in (("mfma", "seg", "pos") if rt == 16 else ("pos",)):
+                m.use_segments = meta in ("seg", "mfma")
+                m.use_mfma = meta == "mfma"
                 m(x, out=y, kernel="tile-lds-exact")
                 torch.cuda.synchronize()
                 if ref is None:
