@@ -1609,7 +1609,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     else NIIDMIX_TLDS_RUN(NIIDMIX_UPD_FAST);
 }
 
-// The RT = 16 segment walker (niidmix.tile.build_tile_segments): ONE asm block walks up to 64 of a
+// The RT = 16 segment walker (niidmix.tile.build_tile_segments): ONE asm block walks all of a
 // tile's segments, so the accumulator tuple stays pinned in v[32:63] from the first segment to the
 // last (one asm statement per segment let the compiler keep the tuple in other registers between
 // them and copy all 16 pairs in and out around every segment: 32 v_mov per segment, ~30 % of the
@@ -1631,30 +1631,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // the remaining rows), s43 dz, s44 weight, s46 skipped row * 2 / row index, s47 position.  VGPR
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
 // saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
-// updates of the first NR = 4, 8, 12 or 16 accumulator pairs (a tile of <= NR rows keeps them in
-// v[32 : 32 + 2 NR); a 100-member clique's full-height tiles are 16 x 6 + 4 rows)
-#define NIIDMIX_PKADD4(T, A, B, C, D)                                                               \
-    "v_pk_add_f32 v[" A "], v[" A "], " T "\n\tv_pk_add_f32 v[" B "], v[" B "], " T "\n\t"          \
-    "v_pk_add_f32 v[" C "], v[" C "], " T "\n\tv_pk_add_f32 v[" D "], v[" D "], " T "\n\t"
-#define NIIDMIX_ADDQ0(T) NIIDMIX_PKADD4(T, "32:33", "34:35", "36:37", "38:39")
-#define NIIDMIX_ADDQ1(T) NIIDMIX_PKADD4(T, "40:41", "42:43", "44:45", "46:47")
-#define NIIDMIX_ADDQ2(T) NIIDMIX_PKADD4(T, "48:49", "50:51", "52:53", "54:55")
-#define NIIDMIX_ADDQ3(T) NIIDMIX_PKADD4(T, "56:57", "58:59", "60:61", "62:63")
-#define NIIDMIX_FMAQ(XD, A, B, C, D)                                                                \
-    NIIDMIX_FMA1("v[" A "]", XD) NIIDMIX_FMA1("v[" B "]", XD) NIIDMIX_FMA1("v[" C "]", XD)            \
-    NIIDMIX_FMA1("v[" D "]", XD)
-#define NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ(XD, "32:33", "34:35", "36:37", "38:39")
-#define NIIDMIX_FMAQ1(XD) NIIDMIX_FMAQ(XD, "40:41", "42:43", "44:45", "46:47")
-#define NIIDMIX_FMAQ2(XD) NIIDMIX_FMAQ(XD, "48:49", "50:51", "52:53", "54:55")
-#define NIIDMIX_FMAQ3(XD) NIIDMIX_FMAQ(XD, "56:57", "58:59", "60:61", "62:63")
-#define NIIDMIX_SEG_MUL(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t"
-#define NIIDMIX_SEG_UPD_EXACT(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADD16("%[pr]")
-#define NIIDMIX_SEG_UPD_EXACT12(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]") NIIDMIX_ADDQ1("%[pr]") NIIDMIX_ADDQ2("%[pr]")
-#define NIIDMIX_SEG_UPD_EXACT8(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]") NIIDMIX_ADDQ1("%[pr]")
-#define NIIDMIX_SEG_UPD_EXACT4(XD) NIIDMIX_SEG_MUL(XD) NIIDMIX_ADDQ0("%[pr]")
-#define NIIDMIX_UPD_FAST12(XD) NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ1(XD) NIIDMIX_FMAQ2(XD)
-#define NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMAQ0(XD) NIIDMIX_FMAQ1(XD)
-#define NIIDMIX_UPD_FAST4(XD) NIIDMIX_FMAQ0(XD)
+#define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
     "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
@@ -1706,10 +1683,24 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     "s_set_gpr_idx_off\n\t"                                                                          \
     "s_branch .Lmsk_loop_%=\n\t"
 #define NIIDMIX_SEG_WALK(UPD, MSK)                                                                   \
-    asm volatile("s_mov_b32 s40, 0\n"                                                                \
-                 ".Lw_next_%=:\n\t"                                                                  \
-                 "s_cmp_ge_u32 s40, %[cnt]\n\t"                                                      \
+    asm volatile("s_mov_b32 s36, %[sb0]\n"                                                           \
+                 ".Lc_next_%=:\n\t"                                                                  \
+                 "s_cmp_ge_u32 s36, %[sb1]\n\t"                                                      \
                  "s_cbranch_scc1 .Lw_end_%=\n\t"                                                     \
+                 "s_sub_u32 s37, %[sb1], s36\n\t"                                                    \
+                 "s_min_u32 s37, s37, 64\n\t"                                                        \
+                 "s_sub_u32 s35, s37, 1\n\t"                                                         \
+                 "v_min_u32 %[vo], %[ln], s35\n\t"                                                   \
+                 "v_add_u32 %[vo], s36, %[vo]\n\t"                                                   \
+                 "v_lshlrev_b32 %[vo], 4, %[vo]\n\t"                                                 \
+                 "global_load_dword %[dx], %[vo], %[sp]\n\t"                                         \
+                 "global_load_dword %[dy], %[vo], %[sp] offset:4\n\t"                                \
+                 "global_load_dword %[dz], %[vo], %[sp] offset:8\n\t"                                \
+                 "s_waitcnt vmcnt(0)\n\t"                                                            \
+                 "s_mov_b32 s40, 0\n"                                                                \
+                 ".Lw_next_%=:\n\t"                                                                  \
+                 "s_cmp_ge_u32 s40, s37\n\t"                                                         \
+                 "s_cbranch_scc1 .Lc_done_%=\n\t"                                                    \
                  "v_readlane_b32 s41, %[dx], s40\n\t"                                                \
                  "v_readlane_b32 s42, %[dy], s40\n\t"                                                \
                  "v_readlane_b32 s43, %[dz], s40\n\t"                                                \
@@ -1742,32 +1733,119 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  "ds_read_b32 %[q1], %[va] offset:4\n\t"                                             \
                  "s_waitcnt lgkmcnt(0)\n\t"                                                          \
                  MSK                                                                                 \
-                 "\n.Lw_end_%=:\n\t"                                                                 \
+                 "\n.Lc_done_%=:\n\t"                                                                \
+                 "s_add_u32 s36, s36, 64\n\t"                                                        \
+                 "s_branch .Lc_next_%=\n"                                                            \
+                 ".Lw_end_%=:\n\t"                                                                   \
                  "s_waitcnt lgkmcnt(0)"                                                              \
                  : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2),             \
                    [x3] "=&v"(x3), [pr] "=&v"(pr), [sv0] "=&v"(sv0), [sv1] "=&v"(sv1),              \
-                   [q0] "=&v"(q0), [q1] "=&v"(q1), [va] "=&v"(va)                                   \
-                 : [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz), [cnt] "s"(cnt), [base] "s"(base),       \
+                   [q0] "=&v"(q0), [q1] "=&v"(q1), [va] "=&v"(va), [dx] "=&v"(dx), [dy] "=&v"(dy),  \
+                   [dz] "=&v"(dz), [vo] "=&v"(vo)                                                   \
+                 : [sp] "s"(segp), [sb0] "s"(sb0), [sb1] "s"(sb1), [ln] "v"(lane), [base] "s"(base), \
                    [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),                          \
                    [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB)             \
-                 : "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "m0", "scc", \
-                   "memory")
-// NR: the tile's rows sit in accumulator pairs 0 .. NR-1 (4, 8, 12 or 16); runs update only those
-template <bool EXACT, int RB, int NR>
-__device__ __forceinline__ void tlds16_walk(Acc16 &acc, int dx, int dy, int dz, int cnt, int base,
-                                            int w0, int w1, int lane8) {
+                 : "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", \
+                   "s47", "m0", "scc", "memory")
+// segp: the segment words (int4 per segment); the tile's segments [sb0, sb1) are fetched 64 at a time
+// INSIDE the asm (lane j: segment j's words), so no VALU address arithmetic sits between the tile's
+// init and its walk -- hipcc otherwise moved the pinned tuple out of v[32:63] to make room for it
+template <bool EXACT, int RB>
+__device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int sb0, int sb1, int base,
+                                            int w0, int w1, int lane8, int lane) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
-    static_assert(NR == 4 || NR == 8 || NR == 12 || NR == 16, "rows in multiples of 4");
     uint64_t x0, x1, x2, x3, pr;
-    uint32_t sv0, sv1, q0, q1, va;
-    if constexpr (EXACT && NR == 16) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
-    else if constexpr (EXACT && NR == 12) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT12, NIIDMIX_MSK_EXACT);
-    else if constexpr (EXACT && NR == 8) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT8, NIIDMIX_MSK_EXACT);
-    else if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT4, NIIDMIX_MSK_EXACT);
-    else if constexpr (NR == 16) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
-    else if constexpr (NR == 12) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST12, NIIDMIX_MSK_FAST);
-    else if constexpr (NR == 8) NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST8, NIIDMIX_MSK_FAST);
-    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST4, NIIDMIX_MSK_FAST);
+    uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
+    if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
+    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
+    (void)pr;
+}
+
+// Tile init of the RT-16 segment kernels in asm: every row's accumulator acc_r = z_r + fl(ws_r x_r)
+// (exact; fast: fma(ws_r, x_r, z_r)), z_r = x_r * 0 -- the self term (model/__init__.py:19-24) --
+// written straight into the pinned tuple v[32:63].  Initialised in C++, the tuple lived in
+// v[0:31] until the walker and was copied into v[32:63] there: 32 extra VGPRs at the peak (90, so
+// only two 7-wave blocks per CU instead of the three the LDS allows).  Rows' LDS reads two ahead.
+template <bool EXACT>
+__device__ __forceinline__ void tlds16_init(Acc16 &acc, int d_slot, int d_ws, int rb, int base, int lane8) {
+    uint64_t x0, x1, t, pr;
+    uint32_t va;
+    if constexpr (EXACT)
+        asm volatile("s_mov_b64 s[46:47], 0\n\t"
+                 "v_readlane_b32 s40, %[ds], 0\n\t""v_readlane_b32 s42, %[dw], 0\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "v_readlane_b32 s40, %[ds], 1\n\t""v_readlane_b32 s44, %[dw], 1\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[32:33], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 2\n\t""v_readlane_b32 s42, %[dw], 2\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[34:35], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 3\n\t""v_readlane_b32 s44, %[dw], 3\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[36:37], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 4\n\t""v_readlane_b32 s42, %[dw], 4\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[38:39], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 5\n\t""v_readlane_b32 s44, %[dw], 5\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[40:41], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 6\n\t""v_readlane_b32 s42, %[dw], 6\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[42:43], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 7\n\t""v_readlane_b32 s44, %[dw], 7\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[44:45], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 8\n\t""v_readlane_b32 s42, %[dw], 8\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[46:47], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 9\n\t""v_readlane_b32 s44, %[dw], 9\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[48:49], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 10\n\t""v_readlane_b32 s42, %[dw], 10\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[50:51], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 11\n\t""v_readlane_b32 s44, %[dw], 11\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[52:53], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 12\n\t""v_readlane_b32 s42, %[dw], 12\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[54:55], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 13\n\t""v_readlane_b32 s44, %[dw], 13\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[56:57], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 14\n\t""v_readlane_b32 s42, %[dw], 14\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[58:59], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 15\n\t""v_readlane_b32 s44, %[dw], 15\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[60:61], %[t], %[pr]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[62:63], %[t], %[pr]\n\t"
+                 : "={v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [t] "=&v"(t), [pr] "=&v"(pr),
+                   [va] "=&v"(va)
+                 : [ds] "v"(d_slot), [dw] "v"(d_ws), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
+                 : "s40", "s42", "s43", "s44", "s45", "s46", "s47", "memory");
+    else
+        asm volatile("s_mov_b64 s[46:47], 0\n\t"
+                 "v_readlane_b32 s40, %[ds], 0\n\t""v_readlane_b32 s42, %[dw], 0\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "v_readlane_b32 s40, %[ds], 1\n\t""v_readlane_b32 s44, %[dw], 1\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[32:33], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 2\n\t""v_readlane_b32 s42, %[dw], 2\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[34:35], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 3\n\t""v_readlane_b32 s44, %[dw], 3\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[36:37], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 4\n\t""v_readlane_b32 s42, %[dw], 4\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[38:39], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 5\n\t""v_readlane_b32 s44, %[dw], 5\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[40:41], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 6\n\t""v_readlane_b32 s42, %[dw], 6\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[42:43], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 7\n\t""v_readlane_b32 s44, %[dw], 7\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[44:45], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 8\n\t""v_readlane_b32 s42, %[dw], 8\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[46:47], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 9\n\t""v_readlane_b32 s44, %[dw], 9\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[48:49], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 10\n\t""v_readlane_b32 s42, %[dw], 10\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[50:51], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 11\n\t""v_readlane_b32 s44, %[dw], 11\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[52:53], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 12\n\t""v_readlane_b32 s42, %[dw], 12\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[54:55], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 13\n\t""v_readlane_b32 s44, %[dw], 13\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[56:57], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 14\n\t""v_readlane_b32 s42, %[dw], 14\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[58:59], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 15\n\t""v_readlane_b32 s44, %[dw], 15\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[60:61], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[62:63], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 : "={v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [t] "=&v"(t), [pr] "=&v"(pr),
+                   [va] "=&v"(va)
+                 : [ds] "v"(d_slot), [dw] "v"(d_ws), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
+                 : "s40", "s42", "s43", "s44", "s45", "s46", "s47", "memory");
     (void)pr;
 }
 
@@ -2067,32 +2145,27 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const int d_slot = sub_slot[sub * RT + li];
         const float d_ws = sub_wself[sub * RT + li];
         TileAcc<RT> acc;
+        if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && (NIIDMIX_TLDS_SPLIT == 0 || NIIDMIX_TLDS_SPLIT == 2)) {
+            tlds16_init<EXACT>(acc.v[0], d_slot, __float_as_int(d_ws), rs * (int)sizeof(f2), (int)lds_base, lane8);
+        } else {
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + sl];
-            const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
-            acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
+            for (int r = 0; r < RT; ++r) {
+                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + sl];
+                const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d_ws), r));
+                acc.set(r, axpy2<EXACT>(ws, xs, xs * 0.f));
+            }
         }
         if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && (NIIDMIX_TLDS_SPLIT == 0 || NIIDMIX_TLDS_SPLIT == 2)) {
             {                                                            // segment loop (tile.py)
                 const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
-                // rows of the tile: pairs 0 .. nr-1 (niidmix.tile fills a tile's slots from the top;
-                // unused slots have row -1 and are never skipped or masked)
-                const int nr = 32 - __builtin_clz((uint32_t)__ballot(lane < RT && d_row >= 0) | 1u);
                 const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
-                for (int sb = sb0; sb < sb1; sb += 64) {
-                    // 64 segments' descriptors lane-parallel (one int4 each), handed out by
-                    // v_readlane: a run: x = first slot | length << 12 | first skipped row << 20,
-                    // y = weight-select bits, z = skip bits; a MASKED position: x = slot | 1 << 30,
-                    // y = the rows that take it, z = its weight (fp32 bits)
-                    const int cnt = sb1 - sb < 64 ? sb1 - sb : 64;
-                    const int4 da = reinterpret_cast<const int4 *>(seg)[sb + (lane < cnt ? lane : cnt - 1)];
-                    constexpr int RB = rs * (int)sizeof(f2);
-                    if (nr <= 4) tlds16_walk<EXACT, RB, 4>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
-                    else if (nr <= 8) tlds16_walk<EXACT, RB, 8>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
-                    else if (nr <= 12) tlds16_walk<EXACT, RB, 12>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
-                    else tlds16_walk<EXACT, RB, 16>(acc.v[0], da.x, da.y, da.z, cnt, (int)lds_base, w0, w1, lane8);
-                }
+                // segment words (int4 each): a run: first slot | length << 12 | first skipped row << 20,
+                // weight-select bits, skip bits; a MASKED position: slot | 1 << 30, the rows that take
+                // it, its weight (fp32 bits).  One walker for every tile: walkers specialised by the
+                // tile's row count (4 / 8 / 12 / 16 pairs) measured no faster, and their four call
+                // sites made hipcc keep a second copy of the tuple (90 VGPRs, two blocks per CU)
+                tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0, w1,
+                                                             lane8, lane);
                 goto tile_epilogue;
             }
         }
