@@ -1919,7 +1919,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
     const int32_t *__restrict__ seg_ptr, const int32_t *__restrict__ seg,
     const float *__restrict__ seg_w, const int32_t *__restrict__ mf_ptr,
-    const int32_t *__restrict__ mf) {
+    const int32_t *__restrict__ mf, int mf_waves) {
     // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
     // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
@@ -2048,8 +2048,41 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 const int row_j = __shfl(d_row, jr), slot_j = __shfl(d_slot, jr);
                 const float ws_j = __shfl(d_ws, jr);
                 float *srow = lds_tile + slot_j * (int)CW + 32 * g4;
+                // waves [0, mf_waves) take the matrix cores, the others the segment walker: the two
+                // pipes run side by side (a wave on either stores its rows itself)
+                const bool mfw = wave < mf_waves;
+                const int64_t colw = c0 + 2 * lane;
+                const bool okw = lane < rs && colw < p;
+                const int slw = lane < rs ? lane : rs - 1;
+                if (have && !mfw) {
+                    typedef __attribute__((address_space(3))) float lds_float_w;
+                    const unsigned lds_base = (unsigned)(size_t)(lds_float_w *)lds_tile;
+                    TileAcc<16> wacc;
+                    const int l8w = slw * (int)sizeof(f2);
+                    tlds16_init<EXACT>(wacc.v[0], d_slot, __float_as_int(d_ws), rs * (int)sizeof(f2),
+                                       (int)lds_base, l8w);
+                    const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
+                    tlds16_walk<EXACT, rs * (int)sizeof(f2)>(wacc.v[0], seg, sb0, sb1, (int)lds_base,
+                                                             __float_as_int(seg_w[2 * sub]),
+                                                             __float_as_int(seg_w[2 * sub + 1]), l8w, lane);
+#pragma unroll
+                    for (int r = 0; r < RT; ++r) {
+                        const int row = __builtin_amdgcn_readlane(d_row, r);
+                        if (row < 0) continue;                               // wave-uniform
+                        f2 o = wacc.get(r);
+                        if (!avg_only) {
+                            const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + slw];
+                            o = xs * 0.f + o;
+                        }
+                        if (okw) {
+                            float *dst = y + (int64_t)row * ld_y + colw;
+                            __builtin_nontemporal_store(o.x, dst);
+                            __builtin_nontemporal_store(o.y, dst + 1);
+                        }
+                    }
+                }
                 f4v acc[8];
-                if (have) {
+                if (have && mfw) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {                            // self: z + fl(ws * xs)
                         const float4 a = *reinterpret_cast<const float4 *>(srow + 8 * r);
@@ -2099,7 +2132,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 // (distinct slots: a group's rows are distinct), then is stored row by row with the
                 // walker's coalesced pattern (lane = column pair).
                 __syncthreads();
-                if (have && row_j >= 0) {
+                if (have && mfw && row_j >= 0) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         if (32 * g4 + 8 * r < (int)CW) {                     // CW: a multiple of 8
@@ -2109,10 +2142,10 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                                 make_float4(acc[4][r], acc[5][r], acc[6][r], acc[7][r]);
                         }
                 }
-                if (have) {
-                    const int64_t col = c0 + 2 * lane;
-                    const bool okc = lane < rs && col < p;
-                    const int slc = lane < rs ? lane : rs - 1;
+                if (have && mfw) {
+                    const int64_t col = colw;
+                    const bool okc = okw;
+                    const int slc = slw;
 #pragma unroll
                     for (int r = 0; r < RT; ++r) {
                         const int row = __builtin_amdgcn_readlane(d_row, r);
@@ -3182,6 +3215,10 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     // matrix-core path (exact mode, segment plans only: the walker is its per-block fallback)
     const bool mf = seg && mode == NIIDMIX_MODE_EXACT && plan->mf_ptr != nullptr;
     if (mf && !plan->mf) return set_error(NIIDMIX_EINVAL, "null MFMA position list");
+    // waves of a block on the matrix cores (the rest walk segments on the VALU side by side);
+    // NIIDMIX_TLDS_MF_WAVES overrides (tuning), default every wave
+    int mf_waves = plan->max_tiles;
+    if (const char *e = getenv("NIIDMIX_TLDS_MF_WAVES")) mf_waves = atoi(e);
     const int stage_rows = plan->max_src + (seg ? 2 : 0);
     if (plan->rt == 16) {
         auto blocks = [&](int c) {
@@ -3207,7 +3244,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
                        : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, false> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, false> : k_mix_tile_lds<E, R, V, 64, false>); \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf, mf_waves); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)

@@ -205,8 +205,9 @@ def test_tile_lds_segment_loop_bitwise(name, gpu, oracle_mod):
         assert ok, (name, worst)
 
 
+@pytest.mark.parametrize("mf_waves", ["", "3"])
 @pytest.mark.parametrize("name", golden_cases())
-def test_tile_lds_mfma_bitwise(name, gpu, oracle_mod):
+def test_tile_lds_mfma_bitwise(name, mf_waves, gpu, oracle_mod, monkeypatch):
     """The exact matrix-core path (v_mfma_f32_16x16x4_f32 with 0/1 row masks; blocks whose staged
     rows hold a non-finite or tiny value fall back to the segment walker; Mixer.use_mfma, off by
     default) is bit-identical to the reference on every golden case, non-finite fixtures included,
@@ -214,6 +215,8 @@ def test_tile_lds_mfma_bitwise(name, gpu, oracle_mod):
     g = load_golden(name)
     if g["x"].shape[1] % 2:
         pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    if mf_waves:      # the first 3 waves of a block on the matrix cores, the rest walk segments
+        monkeypatch.setenv("NIIDMIX_TLDS_MF_WAVES", mf_waves)
     m = _tile_lds_mixer(g, gpu, 16)
     assert m.tmf is not None and m.tmf.lp is m.tlds
     x = torch.from_numpy(g["x"]).to(gpu)
