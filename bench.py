@@ -109,6 +109,18 @@ def parse():
                     help="multi-GPU: rank 0 also times the N=1 point on its own GPU in the same run "
                          "(--config dcliques10000: the whole fixed problem -> speedup_vs_1gpu; "
                          "weak line: nodes_per_gpu nodes -> weak_efficiency_vs_1gpu) (auto: on)")
+    ap.add_argument("--node-legs", default="auto",
+                    help="multi-GPU with --shard stripes: after the stripes line, also time the "
+                         "NODE-SHARD partition (RCCL halo exchange) on the same problem, one leg per "
+                         "interclique in this comma list (auto: --interclique, then smallworld; "
+                         "off: none).  Results go to config.node_shards; a failed or timed-out leg "
+                         "records its error there and the stripes line is still printed")
+    ap.add_argument("--leg-timeout", type=float, default=240.0,
+                    help="multi-GPU: seconds one node-shard leg may take before every rank gives up "
+                         "(rank 0 prints the line with the error, then all ranks exit 0)")
+    ap.add_argument("--pg-timeout", type=float, default=900.0,
+                    help="multi-GPU: torch.distributed collective timeout (seconds), above "
+                         "--leg-timeout so the leg watchdog fires first")
     return ap.parse_args()
 
 
@@ -330,6 +342,138 @@ def timed_rounds(step, xa, xb, steps, warmup, dev, dist=None, use_graph=False, b
     return region_s, launch_ms, graph
 
 
+class LegWatchdog:
+    """Deadline for one multi-GPU leg.  A point-to-point exchange that one rank never joins leaves
+    its peers waiting inside RCCL (no exception reaches Python), so a timer thread ends the run
+    instead: on_fire() (rank 0 prints the line measured so far, with the leg's error) and then
+    exit_fn(0) -- os._exit, the process ends in place (no exec, no retry)."""
+
+    def __init__(self, seconds, on_fire, exit_fn=None):
+        import threading
+        self.on_fire = on_fire
+        self.exit_fn = exit_fn or os._exit
+        self.fired = False
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+
+    def _fire(self):
+        self.fired = True
+        try:
+            self.on_fire()
+        finally:
+            self.exit_fn(0)
+
+    def __enter__(self):
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.cancel()
+        return False
+
+
+def guarded_leg(fn, dist, world, rank, flag_device="cpu"):
+    """Run one leg on every rank; an exception is captured, not raised.  Every rank then learns
+    which ranks failed (one SUM all-reduce of a per-rank flag), so all ranks leave the leg
+    together.  Returns (info, error): info = fn()'s result, or None with error = a string naming
+    the failed ranks and this rank's own exception (if any)."""
+    info, err = None, None
+    try:
+        info = fn()
+    except Exception as e:                               # noqa: BLE001 - recorded in the line
+        err = f"{type(e).__name__}: {e}"
+        print(f"[bench rank {rank}] node-shard leg failed: {err}", file=sys.stderr, flush=True)
+    flags = torch.zeros(world, dtype=torch.float64, device=flag_device)
+    flags[rank] = 1.0 if err else 0.0
+    if dist is not None and world > 1:
+        dist.all_reduce(flags, op=dist.ReduceOp.SUM)
+    failed = [r for r in range(world) if flags[r].item() > 0]
+    if failed:
+        return None, f"failed on rank(s) {failed}" + (f": {err}" if err else "")
+    return info, None
+
+
+def node_shard_leg(make, interclique, steps, warmup, dev, dist, backend, seed=0, single_ms=None,
+                   fixed=False, fill=None):
+    """Time the NODE-SHARD partition on one interclique with bench's own timed loop: `make(ic)`
+    returns this rank's ShardedMixer (whole cliques per rank; every round the rows other ranks read
+    go out and the rows this rank reads come in by grouped point-to-point, batch_isend_irecv =
+    grouped ncclSend / ncclRecv over xGMI, pipelined with the mixing over column windows).  The
+    reference's only exchange design is the same per-edge push (v1 gossip: isend(theta * W) /
+    recv per edge, tools/v1/simulate.py:1570-1602).  fill(sm, x) sets the initial local rows
+    (default: seeded N(0, 1)).  Returns (info, last output slab, mixer)."""
+    sm = make(interclique)
+    xa = sm.empty()
+    if fill is None:
+        gen = torch.Generator(device=dev).manual_seed(seed + 1000 * (sm.rank + 1))
+        xa.normal_(generator=gen)
+    else:
+        fill(sm, xa)
+    xb = sm.empty()
+    kernel = sm.kernel_for("fast", xa)
+    mode = "exact" if str(kernel).endswith("exact") else "fast"
+
+    def step(a, b, evs=None):
+        sm(a, b, kernel=kernel, mode=mode, events=evs)
+    region_s, launch_ms, _ = timed_rounds(step, xa, xb, steps, warmup, dev, dist, False, backend)
+    hb = torch.tensor([sm.halo_bytes, sm.send_bytes, sm.halo_rows], dtype=torch.float64,
+                      device=dev if (backend == "nccl" and dev.type == "cuda") else "cpu")
+    if dist is not None:
+        dist.all_reduce(hb, op=dist.ReduceOp.MAX)
+    ms = region_s * 1e3 / steps
+    info = {"interclique": interclique, "ms_per_step": round(ms, 4),
+            "value_GBs": round(sm.n_total * sm.p * 4 / (ms / 1e3) / 1e9, 2),
+            "launch_ms": round(launch_ms, 4), "kernel": kernel, "mode": mode,
+            "windows": sm.k, "window_cols": sm.w,
+            "halo_rows_max": int(hb[2].item()),
+            "halo_GB_recv_max": round(hb[0].item() / 1e9, 3),
+            "halo_GB_send_max": round(hb[1].item() / 1e9, 3),
+            "exchange": ("per column window: pack rows several peers read (index_select), "
+                         "batch_isend_irecv with every peer (grouped ncclSend/ncclRecv) on a comm "
+                         "stream; the compute stream waits only for that window")}
+    if single_ms:
+        key = "speedup_vs_1gpu" if fixed else "weak_efficiency_vs_1gpu"
+        info[key] = round(single_ms / ms, 3)
+    last = xa if (steps + warmup) % 2 == 0 else xb
+    return info, last, sm
+
+
+def node_leg_intercliques(spec, interclique):
+    if spec == "off":
+        return []
+    if spec == "auto":
+        return [interclique] + (["smallworld"] if interclique != "smallworld" else [])
+    out = [s.strip() for s in spec.split(",") if s.strip()]
+    bad = [s for s in out if s not in ("fully-connected", "smallworld", "ring")]
+    if bad:
+        raise SystemExit(f"--node-legs: unknown interclique(s) {bad}")
+    return out
+
+
+def run_node_legs(make, intercliques, args, world, rank, dev, dist, backend, single_ms, fixed,
+                  report, on_timeout=None, exit_fn=None):
+    """Every node-shard leg, each under its own LegWatchdog and guarded_leg.  `report` is the list
+    the results go into (rank 0's line holds it as config.node_shards); on a timeout the leg's
+    error is appended and on_timeout() (rank 0: print the line as it stands) runs before exit."""
+    flag_dev = dev if (backend == "nccl" and dev.type == "cuda") else "cpu"
+    for ic in intercliques:
+        pending = {"interclique": ic, "error": f"timed out after {args.leg_timeout:.0f} s"}
+
+        def fire():
+            report.append(pending)
+            if on_timeout is not None:
+                on_timeout()
+        with LegWatchdog(args.leg_timeout, fire, exit_fn):
+            info, err = guarded_leg(
+                lambda: node_shard_leg(make, ic, args.steps, args.warmup, dev, dist, backend,
+                                       args.seed, single_ms, fixed)[0],
+                dist, world, rank, flag_dev)
+        report.append(info if err is None else {"interclique": ic, "error": err})
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+    return report
+
+
 def single_gpu_round_ms(n, p, interclique, dev, steps, warmup):
     """One GPU, the whole d-cliques problem of n nodes: the headline kernel on column-blocked VMM
     slabs (2 x n*p*4 bytes), mean of `steps` rounds after `warmup`."""
@@ -481,10 +625,12 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        import datetime
+        pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
 
     from niidmix import memory, ops
     if args.workload != "mix" and world > 1:
@@ -622,6 +768,7 @@ def main():
         dist.barrier()
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
 
+    out = None
     if rank == 0:
         # PMC traffic is profiled per single-GPU config and library build (profiles/traffic.json)
         from niidmix import _lib
@@ -688,7 +835,30 @@ def main():
             else:       # weak: each GPU's work equals the N=1 round's
                 out["config"]["single_gpu_nodes"] = args.nodes_per_gpu
                 out["config"]["weak_efficiency_vs_1gpu"] = round(single / (step_s * 1e3), 3)
-        print(json.dumps(out), flush=True)
+    node_legs = (node_leg_intercliques(args.node_legs, args.interclique)
+                 if world > 1 and args.shard == "stripes" else [])
+    import threading
+    print_lock, printed = threading.Lock(), [False]
+
+    def emit():
+        with print_lock:
+            if out is not None and not printed[0]:
+                printed[0] = True
+                print(json.dumps(out), flush=True)
+    if node_legs:
+        # the same problem again as NODE SHARDS: whole cliques per rank, cross-shard edges' rows
+        # exchanged over RCCL every round; never changes the stripes `value`
+        from niidmix.shard import ShardedMixer
+        legs = []
+        if out is not None:
+            out["config"]["node_shards"] = legs
+
+        def make(ic):
+            return ShardedMixer.dcliques(n_total=n_multi, clique_size=100, world=world, rank=rank,
+                                         interclique=ic, device=dev, p=p, windows=args.windows)
+        run_node_legs(make, node_legs, args, world, rank, dev, dist, backend, single, fixed, legs,
+                      on_timeout=emit)
+    emit()
     if dist:
         dist.destroy_process_group()
 

@@ -124,6 +124,8 @@ def mix_ell(x: torch.Tensor, ell_col: torch.Tensor, ell_val: torch.Tensor, ell_l
     _slab("out", out, cols=x.shape[1])
     _req(out.device == x.device, "x and out must be on the same device")
     n = out.shape[0]
+    # the kernel reads x[row] (the row's own entry) for every output row before its descriptors
+    _req(x.shape[0] >= n, f"x has {x.shape[0]} rows, fewer than the {n} output rows")
     _vec("ell_col", ell_col, torch.int32, x.device, n * k)
     _vec("ell_val", ell_val, torch.float32, x.device, n * k)
     _vec("ell_len", ell_len, torch.int32, x.device, n)

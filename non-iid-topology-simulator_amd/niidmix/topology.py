@@ -87,7 +87,7 @@ def load(rundir):
             comp = os.path.join(rundir, topo.get("weights-csr", CSR_FILE))
             if os.path.exists(comp):
                 csr, _ = load_csr(comp)
-                if csr.n == len(topo["edges"]):
+                if _csr_matches_edges(csr, topo["edges"]):
                     topo["csr"] = csr
             return topo
         if not (os.path.exists(sparse) and os.path.getmtime(sparse) > os.path.getmtime(path)):
@@ -99,6 +99,24 @@ def load(rundir):
             topo["cliques"] = cliques
         return topo
     raise FileNotFoundError(path)
+
+
+def _csr_matches_edges(csr, edges, spot=64):
+    """A companion CSR belongs to these edge lists: same N, nnz = N + sum(len(edges[r])), and the
+    column lists of up to `spot` rows (first, last, evenly spaced) equal [r] + edges[r].  A stale
+    companion (e.g. an interrupted write_sparse / --randomize, which write the CSR before the
+    JSON) is then ignored and to_csr rebuilds the weights from the edges (mh_csr)."""
+    n = len(edges)
+    if csr.n != n or sorted(edges) != list(range(n)):
+        return False
+    if csr.nnz != n + sum(len(edges[r]) for r in range(n)):
+        return False
+    rows = np.unique(np.linspace(0, n - 1, min(n, spot)).astype(np.int64)) if n else []
+    for r in rows:
+        b, e = int(csr.row_ptr[r]), int(csr.row_ptr[r + 1])
+        if csr.col[b:e].tolist() != [int(r)] + [int(c) for c in edges[int(r)]]:
+            return False
+    return True
 
 
 @dataclass
@@ -235,6 +253,11 @@ def _check_stochastic(w):
         "Weights should sum to 1. Sum is off by {}".format(w.sum(axis=1) - 1.0)
 
 
+# below this many nodes a dense row is reduced by one thread either way (ATen's GRAIN_SIZE), so a
+# batched 2-D row sum has the 1-D reduction's order; at or above it mh_csr sums row by row
+ROWSUM_BATCH_MAX = 32768
+
+
 def mh_csr(n, edges):
     """Sparse Metropolis-Hastings straight to the mixing CSR, without materialising the N x N JSON.
     Values are bit-identical to compute_weights (weights.py:15-25):
@@ -271,7 +294,14 @@ def mh_csr(n, edges):
             ri = torch.from_numpy(wi[a:b] - r0)
             ci = torch.from_numpy(wj[a:b])
             buf[ri, ci] = torch.from_numpy(wv[a:b])
-            diag[r0:r1] = (1. - buf[:r1 - r0].sum(1)).numpy()
+            if n < ROWSUM_BATCH_MAX:
+                diag[r0:r1] = (1. - buf[:r1 - r0].sum(1)).numpy()
+            else:
+                # ATen splits a 1-D reduction of >= GRAIN_SIZE (32768) elements over its threads,
+                # so the batched row sum (one thread per row) would order the adds differently:
+                # reduce every dense row on its own, as the reference's W[i, :].sum() does
+                for i in range(r1 - r0):
+                    diag[r0 + i] = float(1. - buf[i].sum())
             buf[ri, ci] = 0.0
     # CSR of W^T in d_sgd.average's operand order: row i = [i] + edges[i]; value W[src, i]
     keys = np.unique(wi * n + wj) if wi.size else np.zeros(0, np.int64)   # W[a, b] != 0 pairs

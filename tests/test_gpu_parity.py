@@ -541,8 +541,8 @@ def test_multi_clique_tile_vs_golden(name, tile, gpu, oracle_mod, monkeypatch):
     g = load_golden(name)
     m = _mixer(g, gpu)
     p = g["x"].shape[1]
-    if m.plan is None or p % 4 or m.plan.max_clique > 104:
-        pytest.skip("no clique plan / p % 4 / clique > 104 members")
+    if m.plan is None or p % 4:
+        pytest.skip("no clique plan / p % 4")
     monkeypatch.setenv("NIIDMIX_CLIQUE_Q", "4")
     monkeypatch.setenv("NIIDMIX_CLIQUE_QT", tile)
     if m.plan.max_clique > 112 or int(tile.split("x")[0]) * int(tile.split("x")[1]) < m.plan.max_clique:
@@ -558,16 +558,19 @@ def test_multi_clique_tile_vs_golden(name, tile, gpu, oracle_mod, monkeypatch):
         assert oracle_mod.bitwise_equal(memory.from_blocked(yb, p).cpu().numpy(), y), (name, tile, bc)
 
 
-@pytest.mark.parametrize("n,inter", [(4000, "fully-connected"), (5000, "smallworld"), (4200, "ring")])
-def test_multi_clique_tile_auto(n, inter, gpu, oracle_mod, monkeypatch):
+@pytest.mark.parametrize("n,inter,size", [(4000, "fully-connected", 100), (5000, "smallworld", 100),
+                                          (4200, "ring", 100), (4400, "smallworld", 110),
+                                          (4480, "fully-connected", 112)])
+def test_multi_clique_tile_auto(n, inter, size, gpu, oracle_mod, monkeypatch):
     """Many cliques (>= 4096 member rows): the launcher picks the multi-clique tile by itself; a
     ragged column tail (p = 4100) and a clique count not divisible by 4 (42 cliques of 100); equal
     within the tolerance to the one-clique tile (NIIDMIX_CLIQUE_Q=1) and to the oracle."""
     from niidmix import memory, ops
     from niidmix.generate import dcliques_csr
-    csr, cliques = dcliques_csr(n, 100, inter, 1337)
+    csr, cliques = dcliques_csr(n, size, inter, 1337)
     m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
     assert m.plan is not None, m.plan_reason
+    assert m.plan.max_clique == size       # 105-112 members: the 16x7 tile on 64-column blocks
     p = 4100
     xh = torch.randn(n, p, generator=torch.Generator().manual_seed(n))
     x = xh.to(gpu)

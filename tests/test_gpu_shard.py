@@ -206,3 +206,29 @@ def test_local_sharded_round_c_abi(world, p, gpu, oracle_mod):
     bound = oracle_mod.condition_bound(xh.numpy(), g["row_ptr"], g["col"], g["val"])
     ok, worst = oracle_mod.check_tolerance(yf, r1, bound, rtol=1e-5)
     assert ok, worst
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_local_sharded_round_rccl_devices(world, gpu, oracle_mod):
+    """The RCCL branch of niidmix_mix_sharded_f32: one shard per DISTINCT GPU (ncclCommInitAll
+    over `world` devices, grouped ncclSend / ncclRecv of the halo rows), two exact rounds bitwise
+    the oracle applied twice.  Needs `world` visible GPUs (skipped on the one-GPU pool boxes; the
+    driver's 8-GPU node runs it)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs, {torch.cuda.device_count()} visible")
+    from niidmix.ops import csr_from_numpy
+    from niidmix.shard import LocalShardedRound
+    g = load_golden("dcliques1000_fc_p64")
+    csr = csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    devs = [torch.device("cuda", i) for i in range(world)]
+    sr = LocalShardedRound(csr, g["cliques"], devs, 4096)
+    assert not sr.loopback
+    xh = torch.randn(1000, 4096, generator=torch.Generator().manual_seed(world))
+    sr.scatter(xh.to(gpu))
+    sr("exact")
+    sr("exact")
+    y = sr.gather().numpy()
+    ref = xh.numpy()
+    for _ in range(2):
+        ref = oracle_mod.mix_exact_c(ref, g["row_ptr"], g["col"], g["val"])
+    assert oracle_mod.bitwise_equal(y, ref)

@@ -177,3 +177,42 @@ def test_sparse_weights_errors():
     with pytest.raises(ValueError, match="every rank"):
         T.to_csr({"edges": {0: [2], 2: [0]}, "weights": [], "weights-kind": T.SPARSE_KIND})
     assert T.to_csr({"edges": {}, "weights": torch.tensor([])}).n == 0
+
+
+def test_stale_companion_csr_is_ignored(tmp_path):
+    """A sparse topology.json whose companion CSR has the same N but other edges (an interrupted
+    write_sparse / --randomize writes the CSR first) does not get the CSR attached: to_csr then
+    rebuilds the MH weights from the edges it does list."""
+    from niidmix import generate
+    csr_a, edges_a = generate.random_graph_csr(60, 4, 11)
+    csr_b, _ = generate.random_graph_csr(60, 4, 12)
+    T.write_sparse(str(tmp_path), csr_a, edges_a)
+    assert "csr" in T.load(str(tmp_path))
+    T.save_csr(str(tmp_path / "topology.csr.npz"), csr_b)        # stale companion, same N
+    topo = T.load(str(tmp_path))
+    assert "csr" not in topo
+    back = T.to_csr(topo)
+    np.testing.assert_array_equal(back.col, csr_a.col)
+    assert np.array_equal(back.val.view(np.uint32), csr_a.val.view(np.uint32))
+
+
+def test_mh_diag_large_n_matches_dense_row_sum():
+    """At N >= 32768 ATen reduces a 1-D row over several threads; mh_csr then reduces every dense
+    row on its own (ROWSUM_BATCH_MAX), as the reference's W[i, :].sum() (weights.py:25)."""
+    n = T.ROWSUM_BATCH_MAX + 7232                                    # 40 000
+    rng = np.random.default_rng(3)
+    edges = {i: set() for i in range(n)}
+    for i in range(n):
+        for j in rng.integers(0, n, 3):
+            if j != i:
+                edges[i].add(int(j))
+                edges[int(j)].add(i)
+    edges = {i: sorted(e) for i, e in edges.items()}
+    csr = T.mh_csr(n, edges)
+    deg = [len(edges[i]) for i in range(n)]
+    for i in (0, 1, n // 2, n - 1):
+        row = torch.zeros(n)
+        for j in edges[i]:
+            row[j] = 1. / (max(deg[i], deg[j]) + 1)
+        want = (1. - row.sum()).numpy()
+        assert csr.val[csr.row_ptr[i]].view(np.uint32) == np.float32(want).view(np.uint32), i
