@@ -68,7 +68,8 @@ def parse():
                              "dcliques10000"])
     ap.add_argument("--p", type=int, default=None, help="parameters per node (default per config)")
     ap.add_argument("--kernel", default="auto",
-                    choices=["auto", "csr-exact", "csr-fast", "ell-exact", "ell-fast", "clique", "dense", "tile-exact",
+                    choices=["auto", "csr-exact", "csr-fast", "ell-exact", "ell-fast", "band-exact",
+                             "band-fast", "clique", "dense", "tile-exact",
                              "tile-fast", "tile-lds-exact", "tile-lds-fast"])
     ap.add_argument("--interclique", default="fully-connected",
                     choices=["fully-connected", "smallworld", "ring"],
@@ -84,6 +85,10 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident round (pinned [N,P] host slab -> H2D -> mix -> "
                          "D2H, pipelined over column windows: the drop-in's per-round cost)")
+    ap.add_argument("--e2e-step", action="store_true",
+                    help="also time the drop-in's WHOLE round (d_sgd.next_step: CPU training of every "
+                         "node, optimizer steps, mixing) with and without the mixing, and report the "
+                         "mixing's exposed cost per round (row-streamed / windowed)")
     ap.add_argument("--layout", default="blocked", choices=["blocked", "blocked-rank", "rowmajor"],
                     help="single GPU, clique kernel: device-resident slabs column-blocked [P/B, N, B] "
                          "with clique-contiguous rows and B per plan (Mixer.device_layout, default), "
@@ -267,6 +272,100 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
         ts.append(time.perf_counter() - t0)
     res["unfused_exact_round_ms"] = round(float(np.median(ts)) * 1e3, 2)
     res["window_cols"] = w
+    return res
+
+
+def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
+    """The drop-in's whole round, d_sgd.next_step (d_sgd.py:178-254) on the same topology: N nodes
+    training on the CPU (synthetic data, a Linear(1023, 1024) model = 2^20 fp32 parameters, batch
+    16), each node's optimizer.step(), then the mixing.  Variants, each timed over `rounds` rounds
+    after one warm-up round (median per round):
+      cpu_only        the same rounds with the mixing removed (the CPU part of the round);
+      row_streamed    the plugin's default: rows go H2D right after their optimizer.step(), the
+                      mixed rows come back while the next round trains (deferred write-back);
+      row_streamed_sync   the same, but next_step waits for every mixed row before returning;
+      windowed        the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0).
+    exposed_ms = round - cpu_only (the mixing's cost the round still pays); host_blocked_ms = the
+    time next_step itself spent waiting for rows or enqueueing copies and kernels (d_sgd.round_stats)."""
+    from niidmix import d_sgd
+    n = csr.n
+    edges = csr.edges()
+    topo = {"edges": edges, "weights": torch.from_numpy(csr.dense())}
+    if cliques:
+        topo["cliques"] = cliques
+    in_f, out_f, batch = 1023, 1024, 16
+    g = torch.Generator().manual_seed(11)
+    data = [(torch.randn(in_f, generator=g), int(torch.randint(0, out_f, (1,), generator=g)))
+            for _ in range(batch * (rounds + 3))]
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(in_f, out_f)
+
+        def forward(self, x, params):
+            return torch.nn.functional.log_softmax(self.fc(x), dim=1)
+
+    def run(variant):
+        env_old = {k: os.environ.get(k) for k in ("NIIDMIX_RESIDENT",)}
+        if variant == "windowed":
+            os.environ["NIIDMIX_RESIDENT"] = "0"
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "topology": {"name": "d-cliques"},
+                  "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 0,
+                             "log-consensus-distance": False},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": batch,
+                                "initial-averaging": False, "clique-gradient": False,
+                                "unbiased-gradient": False, "mixing-mode": mode,
+                                "deferred-writeback": variant == "row_streamed"}}
+        torch.manual_seed(3)
+        nodes = []
+        for r in range(n):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data, "model": mdl,
+                          "optimizer": d_sgd.optimizer(mdl, params)})
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if variant == "cpu_only":
+            d_sgd.average = lambda nds, t, p: None
+            d_sgd._row_streamed = lambda p: False
+        ts = []
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for k in range(rounds + 1):
+                if k == 1:
+                    for key in d_sgd.round_stats:
+                        d_sgd.round_stats[key] = 0
+                t0 = time.perf_counter()
+                state, _, _, _ = d_sgd.next_step(state, params, None)
+                ts.append(time.perf_counter() - t0)
+            d_sgd.synchronize()
+            st = dict(d_sgd.round_stats)
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+            for k, v in env_old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            d_sgd._engines.clear()
+        del nodes, state
+        torch.cuda.empty_cache()
+        t = float(np.median(ts[1:]))
+        out = {"round_ms": round(t * 1e3, 1), "round_ms_min": round(min(ts[1:]) * 1e3, 1)}
+        if variant.startswith("row_streamed") and st["rounds"]:
+            out["host_blocked_ms"] = round((st["wait_s"] + st["enqueue_s"]) / rounds * 1e3, 2)
+            out["host_wait_ms"] = round(st["wait_s"] / rounds * 1e3, 2)
+        return out
+
+    res = {"nodes": n, "p": in_f * out_f + out_f, "model": f"Linear({in_f}, {out_f})",
+           "batch": batch, "rounds_timed": rounds, "mode": mode, "threads": torch.get_num_threads()}
+    for v in ("cpu_only", "row_streamed", "row_streamed_sync", "windowed", "cpu_only"):
+        r = run(v)
+        print(f"[bench --e2e-step] {v}: {r}", file=sys.stderr, flush=True)
+        key = v if v not in res else v + "_again"
+        res[key] = r
+    base = min(res["cpu_only"]["round_ms"], res["cpu_only_again"]["round_ms"])
+    for v in ("row_streamed", "row_streamed_sync", "windowed"):
+        res[v]["exposed_ms"] = round(res[v]["round_ms"] - base, 1)
     return res
 
 
@@ -665,6 +764,15 @@ def main():
         if k0 == "auto":
             k0 = mixer.kernel_for("fast") if args.workload == "mix" else "grad-segment-mean"
         row_order = "rank"
+        if args.layout == "blocked" and args.workload == "mix" and args.kernel in ("auto", "band-fast",
+                                                                                 "band-exact"):
+            perm, _ = mixer.device_layout() if mixer.plan is None else (None, None)
+            if perm is not None:
+                # a ring in its cycle order: every row's neighbours are the rows next to it, so the
+                # band kernel reads them without descriptors (Mixer.device_layout)
+                mixer = mixer.relabeled(perm)
+                row_order = "ring cycle order"
+                k0 = mixer.kernel_for("fast")
         if (args.layout in ("blocked", "blocked-rank") and not args.hipmalloc_slabs and p % 4 == 0
                 and ((k0 == "clique" and args.workload == "mix" and mixer.plan.max_clique <= 1024)
                      or args.workload == "grad-clique")):
@@ -754,7 +862,8 @@ def main():
     value = n_total * p * 4 / step_s / 1e9
     slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}], "
                    f"{row_order} rows" if xa.dim() == 3 and (blocked or args.shard == "stripes") else
-                   "window-blocked [K, rows_in, w]" if xa.dim() == 3 else "row-major [N, P]")
+                   "window-blocked [K, rows_in, w]" if xa.dim() == 3 else
+                   "row-major [N, P]" + (f", {row_order} rows" if row_order != "rank" else ""))
     single = None
     if world > 1 and args.single_ref != "off":
         # the N=1 point of this line, measured in the same run on rank 0's GPU with the same
@@ -795,6 +904,11 @@ def main():
             e2e = e2e_fused_rounds(mixer, plan, csr, cliques, n_local, p, dev)
         elif world == 1 and args.e2e:
             e2e = e2e_rounds(mixer, n_local, p, dev)
+        if world == 1 and args.e2e_step and csr is not None:
+            xa = xb = None                              # noqa: F841 (free the device slabs)
+            torch.cuda.empty_cache()
+            e2e = dict(e2e or {})
+            e2e["next_step"] = e2e_next_step(csr, cliques, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config != "dcliques10000":
             if args.workload == "grad-clique":

@@ -22,7 +22,9 @@
  * overlap.  Every entry point that reads one slab and writes another gets the row count and checks
  * the full extents of both (NIIDMIX_EALIAS), each slab with its own strides.
  *
- * ABI 3 (this header): n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
+ * ABI 4 (this header): niidmix_mix_band_f32 added (banded low-degree graphs, e.g. a ring in its
+ * cycle order).
+ * ABI 3: n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
  * niidmix_grad_segment_mean_f32 and niidmix_grad_segment_mean_blocked_f32 (full extent checks);
  * niidmix_update_rows_f32 added (the 'sample' topology's broadcast); niidmix_mix_ell_f32 added
  * (low-degree graphs); niidmix_sharded_* / niidmix_mix_sharded_f32 added (sharded round over
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define NIIDMIX_ABI_VERSION 3
+#define NIIDMIX_ABI_VERSION 4
 
 enum niidmix_status {
     NIIDMIX_OK = 0,
@@ -113,6 +115,20 @@ int niidmix_mix_csr_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                         int64_t p, int k, const int32_t *ell_col, const float *ell_val,
                         const int32_t *ell_len, int mode, void *stream);
+
+/* The same round for BANDED rows: every entry of row r reads row r + d (mod n_rows) with
+ * |d| <= band (a ring in its cycle order: band 1; niidmix.ops.band_layout finds that order and
+ * MixCSR.relabel puts the slab in it).  The descriptors are the ELL arrays of niidmix_mix_ell_f32
+ * (absolute columns, self first, padded to k); the caller guarantees the band (the kernel folds
+ * (col - r) mod n_rows into [-band, band]; an entry outside the band reads a wrong row).  A wave
+ * loads its output rows and the band rows around them before any descriptor arrives, so a round is
+ * one memory round trip per wave and each row is loaded about once instead of k times.
+ * (k, band): (3, 1) or (5, 2); n_rows >= 2 band + 1; p and both ld even, 8-B aligned slabs
+ * (NIIDMIX_EUNSUPPORTED otherwise: use niidmix_mix_ell_f32).  x and y: [n_rows, ld].  mode as
+ * niidmix_mix_ell_f32; bit-identical to it (and to niidmix_mix_csr_f32) in EXACT mode. */
+int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                         int64_t p, int k, int band, const int32_t *ell_col, const float *ell_val,
+                         const int32_t *ell_len, int mode, void *stream);
 
 /* Clique-factored mixing (fast mode only).  For each member m of clique c:
  *   y_m = a_m * x_m + sum_{g < n_groups} c_{m,g} * S_{c,g} + sum_r res_val[r] * x[res_col[r]]

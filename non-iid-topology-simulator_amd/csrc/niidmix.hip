@@ -360,6 +360,111 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 }
 
 // ----------------------------------------------------------------------------------------------
+// Banded low-degree graphs (a ring in its cycle order: every entry of row r is a row r + d, |d| <=
+// B, taken cyclically).  The ELL kernel above is a chain per wave — descriptor load, then the
+// gathers it names, then the store — and reads every row K times.  Here a wave owns R consecutive
+// output rows of CH column chunks and loads the R + 2B rows they can read straight away: the
+// addresses need no descriptor, so the row loads and the scalar descriptor loads are in flight
+// together (one memory round trip per wave), every row is loaded (R + 2B) / R times instead of K,
+// and the operands come out of registers.  The descriptors are the ELL arrays of the same rows
+// (absolute columns; the kernel takes d = (col - r) mod n folded into [-B, B], which the host
+// checked for every entry).  Arithmetic and operand order as k_mix_ell (exact: bit-identical).
+// Work order is XCD-aware: the row groups of one column slice run on one XCD, so the 2B rows a
+// wave shares with its neighbours come from that XCD's L2.
+template <bool EXACT, int VW, int K, int B, int R, int CH>
+__global__ __launch_bounds__(256) void k_mix_band(const float *__restrict__ x, int64_t ld_x,
+                                                  float *__restrict__ y, int64_t ld_y, int64_t n_rows,
+                                                  int64_t p, const int32_t *__restrict__ ell_col,
+                                                  const float *__restrict__ ell_val,
+                                                  const int32_t *__restrict__ ell_len,
+                                                  int64_t n_row_groups, int64_t n_items, int avg_only) {
+    constexpr int NR = R + 2 * B;             // rows loaded per wave
+    constexpr int64_t CW = 64 * VW;           // columns per chunk
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t t = blockIdx.x;
+    if (t >= n_items) return;
+    const int64_t xcd = t & 7, local = t >> 3;
+    const int64_t slice = (local / n_row_groups) * 8 + xcd;
+    const int64_t r0 = ((local % n_row_groups) * 4 + wave) * R;    // first output row of the wave
+    const int64_t c_beg = slice * CH * CW;
+    if (r0 >= n_rows || c_beg >= p) return;   // wave-uniform
+    int64_t cs[CH];
+    bool ok[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int64_t cq = c_beg + c * CW + VW * lane;
+        ok[c] = cq < p;                       // p % VW == 0: a slot is all-in or all-out
+        cs[c] = ok[c] ? cq : 0;
+    }
+    // every row the wave can read, no descriptor needed: rows r0 - B .. r0 + R - 1 + B (cyclic)
+    float xv[NR][CH][VW];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        int64_t ri = r0 - B + i;               // cyclic; n_rows may be < NR (no 64-bit modulo)
+        while (ri < 0) ri += n_rows;
+        while (ri >= n_rows) ri -= n_rows;
+        const float *src = x + ri * ld_x;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) ldv<VW>(src + cs[c], xv[i][c]);
+    }
+    // descriptors by scalar loads, in flight with the row loads
+    int colj[R][K];
+    float valj[R][K];
+    int len[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int64_t r = r0 + j < n_rows ? r0 + j : r0;
+        len[j] = ell_len[r];
+#pragma unroll
+        for (int e = 0; e < K; ++e) {
+            colj[j][e] = ell_col[r * K + e];
+            valj[j][e] = ell_val[r * K + e];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int64_t r = r0 + j;
+        if (r >= n_rows) break;               // wave-uniform
+        float *dst = y + r * ld_y;
+        // d of every entry, folded into [-B, B] (the host checked the band)
+        int dj[K];
+#pragma unroll
+        for (int e = 0; e < K; ++e) {
+            int64_t d = (int64_t)colj[j][e] - r;
+            d = d < 0 ? d + n_rows : d;        // [0, n)
+            dj[e] = (int)(d > B ? d - n_rows : d);
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            float z[VW], acc[VW];
+#pragma unroll
+            for (int v = 0; v < VW; ++v) { z[v] = xv[j + B][c][v] * 0.f; acc[v] = z[v]; }   // self * 0
+#pragma unroll
+            for (int e = 0; e < K; ++e)
+                if (e < len[j]) {                                                 // wave-uniform
+                    float xe[VW];
+#pragma unroll
+                    for (int v = 0; v < VW; ++v) xe[v] = xv[j + B][c][v];
+#pragma unroll
+                    for (int d = -B; d <= B; ++d)
+                        if (d != 0 && dj[e] == d) {                                // uniform select
+#pragma unroll
+                            for (int v = 0; v < VW; ++v) xe[v] = xv[j + B + d][c][v];
+                        }
+                    const float w = valj[j][e];
+#pragma unroll
+                    for (int v = 0; v < VW; ++v) acc[v] = axpy<EXACT>(w, xe[v], acc[v]);
+                }
+            float o[VW];
+#pragma unroll
+            for (int v = 0; v < VW; ++v) o[v] = avg_only ? acc[v] : z[v] + acc[v];
+            if (ok[c]) stv_nt<VW>(dst + cs[c], o);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Clique-factored mixing (fast mode).  Work item = (clique, 256-column chunk); WAVES waves; wave w
 // holds members w, w+WAVES, w+2*WAVES, ... (RPW rows per wave, one float4 per lane per row) in
 // registers.
@@ -3158,6 +3263,57 @@ int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 #undef NIIDMIX_ELL_C
 #undef NIIDMIX_ELL
     return check_launch("k_mix_ell");
+}
+
+int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                         int64_t p, int k, int band, const int32_t *ell_col, const float *ell_val,
+                         const int32_t *ell_len, int mode, void *stream) {
+    if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE);
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (!((k == 3 && band == 1) || (k == 5 && band == 2)))
+        return set_error(NIIDMIX_EUNSUPPORTED, "band kernel: (k, band) = (%d, %d), (3, 1) or (5, 2) supported", k, band);
+    if (n_rows == 0 || p == 0) return NIIDMIX_OK;
+    if (n_rows < 2 * band + 1) return set_error(NIIDMIX_EUNSUPPORTED, "band %d needs >= %d rows", band, 2 * band + 1);
+    if (!x || !y || !ell_col || !ell_val || !ell_len) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    const int vw = (p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && (align & 15) == 0) ? 4
+                 : (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
+    if (vw == 1) return set_error(NIIDMIX_EUNSUPPORTED, "band kernel needs even p and ld, 8-B aligned slabs");
+    // rows per wave x column chunks per wave (R x CH): NIIDMIX_BAND_RC = "R,CH" among the built
+    // shapes (tuning); default 4 x 4
+    int rr = 4, ch = 4;
+    if (const char *e = getenv("NIIDMIX_BAND_RC")) {
+        int a = 0, b = 0;
+        if (sscanf(e, "%d,%d", &a, &b) == 2 &&
+            ((a == 1 && (b == 1 || b == 2 || b == 4)) || (a == 2 && (b == 1 || b == 2)) ||
+             (a == 4 && (b == 1 || b == 4)) || (a == 8 && b == 2))) { rr = a; ch = b; }
+    }
+    const int64_t n_slices = (p + 64 * vw * ch - 1) / (64 * vw * ch);
+    const int64_t n_row_groups = (n_rows + 4 * rr - 1) / (4 * rr);
+    const int64_t n_items = n_row_groups * ((n_slices + 7) / 8) * 8;
+    if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (rows, slice) items");
+    const dim3 grid((unsigned)n_items), block(256);
+#define NIIDMIX_BAND(E, V, KK, BB, RR, C) hipLaunchKernelGGL((k_mix_band<E, V, KK, BB, RR, C>), grid, block, 0, s, x, ld_x, y, ld_y, n_rows, p, ell_col, ell_val, ell_len, n_row_groups, n_items, avg_only)
+#define NIIDMIX_BAND_R(E, V, KK, BB) do { \
+        if (rr == 1) { if (ch == 1) NIIDMIX_BAND(E, V, KK, BB, 1, 1); else if (ch == 2) NIIDMIX_BAND(E, V, KK, BB, 1, 2); else NIIDMIX_BAND(E, V, KK, BB, 1, 4); } \
+        else if (rr == 2) { if (ch == 1) NIIDMIX_BAND(E, V, KK, BB, 2, 1); else NIIDMIX_BAND(E, V, KK, BB, 2, 2); } \
+        else if (rr == 4) { if (ch == 1) NIIDMIX_BAND(E, V, KK, BB, 4, 1); else NIIDMIX_BAND(E, V, KK, BB, 4, 4); } \
+        else NIIDMIX_BAND(E, V, KK, BB, 8, 2); } while (0)
+#define NIIDMIX_BAND_K(E, V) do { if (k == 3) NIIDMIX_BAND_R(E, V, 3, 1); else NIIDMIX_BAND_R(E, V, 5, 2); } while (0)
+#define NIIDMIX_BAND_V(E) do { if (vw == 4) NIIDMIX_BAND_K(E, 4); else NIIDMIX_BAND_K(E, 2); } while (0)
+    if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_BAND_V(true); else NIIDMIX_BAND_V(false);
+#undef NIIDMIX_BAND_V
+#undef NIIDMIX_BAND_K
+#undef NIIDMIX_BAND_R
+#undef NIIDMIX_BAND
+    return check_launch("k_mix_band");
 }
 
 int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NIIDMIX_LIB", os.path.join(_HERE, "libniidmix.so"))
 
 OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
 MODE_EXACT, MODE_FAST = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
 
@@ -61,6 +61,8 @@ SIGNATURES = {
                                            ctypes.c_int, _vp]),
     "niidmix_mix_ell_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp, _vp,
                                            _vp, ctypes.c_int, _vp]),
+    "niidmix_mix_band_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int,
+                                            ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,

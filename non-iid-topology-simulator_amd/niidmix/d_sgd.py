@@ -25,6 +25,7 @@ import itertools
 import json
 import logging
 import os
+import time
 from random import Random
 
 import torch
@@ -138,6 +139,7 @@ def sample_average(all_nodes, active):
     avg = setup.model.average([active models], [1/len(active)]*len(active)), then
     update_models([every model], avg) — one device round over the pinned slab of every node
     (niidmix.slab.SampleAverage), bit for bit the reference's CPU arithmetic."""
+    synchronize()
     key = id(all_nodes)
     eng = _sample_engines.get(key)
     if eng is None or not eng.owns(all_nodes):
@@ -158,6 +160,7 @@ def gradient(nodes, topology, params):
     neighbourhoods), bit-identical to average_gradients + update_gradients; the optimizer steps stay
     on the CPU, on the nodes the reference steps (niidmix.gradient.GradPlan.stepped)."""
     logging.info("  applying gradients")
+    synchronize()
     if not _averages_gradients(params):
         for n in nodes:
             n["optimizer"].step()
@@ -224,6 +227,7 @@ def fused_round(nodes, topology, params):
     """gradient(nodes, topology, params) followed by average(nodes, topology, params), as one
     device round: gradient mean, SGD step and mixing on each column window, one H2D of parameters
     and gradients and one D2H of the mixed parameters (niidmix.slab.FusedRoundRunner)."""
+    synchronize()
     key = id(nodes)
     eng = _fused_engines.get(key)
     if eng is None or not eng.valid_for(nodes, topology, params):
@@ -244,13 +248,19 @@ def _window():
 
 
 class _Engine:
-    """NodeSlab + Mixer + SlabMixer for one (node list, topology) pair.  With several GPUs
-    visible (niidmix.slab.mixing_devices) the round is split into parameter-column stripes, one per
-    GPU, each streamed over its own PCIe link (niidmix.slab.MultiDeviceRound); bitwise the same."""
+    """NodeSlab + Mixer + the round runner for one (node list, topology) pair.
+
+    Resident (default when the two [N, P] buffers fit in HBM, NIIDMIX_RESIDENT=0 disables): the
+    slab stays in HBM and the PCIe copies overlap the CPU part of the round
+    (niidmix.slab.ResidentRound: rows go up right after their optimizer.step(), the mixed rows come
+    back block by block while the next round trains).  Otherwise a windowed round
+    (niidmix.slab.SlabMixer: H2D / mix / D2H pipelined over column windows).  With several GPUs
+    visible (niidmix.slab.mixing_devices) either is split into parameter-column stripes, one per GPU
+    and PCIe link; bitwise the same."""
 
     def __init__(self, nodes, topology, devices):
         from .ops import Mixer
-        from .slab import MultiDeviceRound, NodeSlab, SlabMixer
+        from .slab import MultiDeviceRound, NodeSlab, ResidentRound, SlabMixer
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
         self.slab = NodeSlab([n["model"] for n in nodes])
@@ -259,12 +269,46 @@ class _Engine:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
         self.devices = devices
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
-        self.runner = MultiDeviceRound(
-            lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
-                                           n, cols, dev, window=_window()),
-            self.slab.n, self.slab.p, devices)
+        n, p = self.slab.n, self.slab.p
+        self.resident = None
+        self.runner = None
+        if os.environ.get("NIIDMIX_RESIDENT", "1") != "0" and ResidentRound.fits(n, p, devices):
+            self.resident = ResidentRound(
+                lambda dev: self.mixer if dev == devices[0] else self.mixer.to(dev), n, p, devices,
+                block=int(os.environ.get("NIIDMIX_ROW_BLOCK", 8)))
+        else:
+            self.runner = MultiDeviceRound(
+                lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
+                                               n, cols, dev, window=_window()), n, p, devices)
 
-    def mix(self, mode, timing):
+    # the row-streamed round (resident engine only)
+    def begin_round(self):
+        if self.resident is not None:
+            self.resident.begin(self.slab.host)
+
+    def row_ready(self, i):
+        if self.resident is not None:
+            self.resident.row_ready(i)
+
+    def wait_row(self, i):
+        if self.resident is not None:
+            self.resident.wait_row(i)
+
+    def wait_all(self):
+        if self.resident is not None:
+            self.resident.wait_all()
+
+    def mix(self, mode, timing, defer=False):
+        """One mixing round of every node.  defer=True (resident engine, next_step only): return
+        with the mixed rows still streaming back (wait_row / wait_all before reading them)."""
+        if self.resident is not None:
+            if self.resident.host is None:
+                self.resident.begin(self.slab.host)    # no row streamed: all of them go up now
+            self.resident.mix(mode, timing=timing)
+            if not defer:
+                self.resident.wait_all()
+                return self.resident.last_timing
+            return None
         self.runner.run(self.slab.host, mode=mode, timing=timing)
         return self.runner.last_timing
 
@@ -284,10 +328,14 @@ class _Engine:
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=self.devices[0])
-        for runner in self.runner.runners:
-            if runner is not None:
-                runner.mixer = self.mixer if runner.device == self.devices[0] else \
-                    self.mixer.to(runner.device)
+        if self.resident is not None:
+            for pt in self.resident.parts:
+                pt["mixer"] = self.mixer if pt["dev"] == self.devices[0] else self.mixer.to(pt["dev"])
+        else:
+            for runner in self.runner.runners:
+                if runner is not None:
+                    runner.mixer = self.mixer if runner.device == self.devices[0] else \
+                        self.mixer.to(runner.device)
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
 
@@ -303,22 +351,80 @@ def _mode(params):
     return mode
 
 
-def average(nodes, topology, params):
-    """Every node's model <- sum_j W[j, rank] model_j over [self] + edges[rank], computed from the
-    pre-round models (Jacobi) then written back (update_models), as d_sgd.py:96-116 — one GPU pass
-    over the whole [N, P] slab instead of N*(deg+1)*n_tensors ATen calls."""
-    logging.info("  computing averages of models (GPU, %s)", _mode(params))
+def synchronize():
+    """Wait until the mixed parameters of the last round are all back in the nodes' models.
+    next_step may return while they stream back (deferred write-back, _deferred_ok); everything in
+    this module that reads or writes the models waits first, and so must any other reader."""
+    for eng in _engines.values():
+        eng.wait_all()
+
+
+def _engine(nodes, topology):
     key = id(nodes)
     eng = _engines.get(key)
     if eng is not None and not eng.valid_for(nodes, topology) and eng.owns(nodes):
         eng.set_topology(topology)                   # same nodes, new graph: keep the slab
     if eng is None or not eng.valid_for(nodes, topology):
+        synchronize()
         eng = _Engine(nodes, topology, _devices(nodes))
         _engines.clear()
         _engines[key] = eng
+    return eng
+
+
+def average(nodes, topology, params):
+    """Every node's model <- sum_j W[j, rank] model_j over [self] + edges[rank], computed from the
+    pre-round models (Jacobi) then written back (update_models), as d_sgd.py:96-116 — one GPU pass
+    over the whole [N, P] slab instead of N*(deg+1)*n_tensors ATen calls.  Returns with every model
+    updated."""
+    logging.info("  computing averages of models (GPU, %s)", _mode(params))
+    eng = _engine(nodes, topology)
     t = eng.mix(_mode(params), logging.getLogger().isEnabledFor(logging.INFO))
     if t:
         logging.info("  mixing round: %s", t)
+
+
+# seconds the CPU spent on the mixing in the row-streamed rounds (bench.py --e2e-step): waiting for
+# rows (wait_row / wait_all) and enqueueing copies and kernels (row_ready / mix)
+round_stats = {"wait_s": 0.0, "enqueue_s": 0.0, "rounds": 0}
+
+
+def _row_streamed(params):
+    """Plain D-SGD rounds run row-streamed (next_step drives the resident engine itself instead of
+    gradient() + average(); NIIDMIX_ROW_STREAM=0 restores the two calls)."""
+    return os.environ.get("NIIDMIX_ROW_STREAM", "1") != "0"
+
+
+def _should_log(node, epoch_done, params, state):
+    """run.py:19-25, the driver's test for reading a node's model after next_step."""
+    lg = params.get("logger", {})
+    if lg.get("accuracy-logging-interval") and epoch_done and \
+            node["epoch"] % lg["accuracy-logging-interval"] == 0:
+        return True
+    if lg.get("accuracy-logging-interval-steps") and \
+            state["step"] % lg["accuracy-logging-interval-steps"] == 0:
+        return True
+    return False
+
+
+def _deferred_ok(params, state, epoch_done, active):
+    """May next_step return before the mixed rows are back on the host?  Only when the plugin was
+    registered with deferred write-back (params.algorithm.deferred-writeback, the CLI default;
+    NIIDMIX_DEFERRED_WRITEBACK=0/1 overrides) AND the driver reads no model before the next
+    next_step: run.py:105-119 reads models only through log.state (should_log, run.py:19-25, per
+    active node or node 0 for fully-connected / sample) and log_consensus_distance (every node
+    epoch-done), both predicted here from the same params and state.  The next round's training
+    waits for each node's own rows (wait_row) before its forward."""
+    env = os.environ.get("NIIDMIX_DEFERRED_WRITEBACK")
+    on = (env != "0") if env is not None else bool(params["algorithm"].get("deferred-writeback"))
+    if not on:
+        return False
+    lg = params.get("logger", {})
+    if lg.get("log-consensus-distance") and epoch_done and all(epoch_done.values()):
+        return False
+    if params["topology"]["name"] in ("fully-connected", "sample"):
+        return not _should_log(state["nodes"][0], epoch_done.get(0, False), params, state)
+    return not any(_should_log(n, epoch_done[n["rank"]], params, state) for n in active)
 
 
 def _devices(nodes):
@@ -349,6 +455,7 @@ def _loader(node, params):
 
 def init(nodes, topology, params):
     logging.basicConfig(level=getattr(logging, params["meta"]["log"].upper(), None))
+    synchronize()
     state = {"nodes": nodes, "topology": topology, "step": 0}
     for n in nodes:
         n["train-iterator"] = _loader(n, params)
@@ -429,8 +536,19 @@ def next_step(state, params, rundir):
     sample = params["topology"]["name"] == "sample"
     active = get_sample(state, params, state["step"]) if sample else state["nodes"]
     topology = state["topology"]
+    # plain D-SGD (own gradient, then mixing): the row-streamed round — each node's rows go to the
+    # GPU right after its optimizer.step() and come back while the next round trains
+    streamed = not sample and not _averages_gradients(params) and _row_streamed(params)
+    eng = _engine(active, topology) if streamed else None
+    if eng is None:
+        synchronize()
     losses, epoch_done = {}, {}
-    for node in active:                                   # local training (CPU)
+    clock = time.perf_counter
+    for i, node in enumerate(active):                     # local training (CPU)
+        if eng is not None:
+            t0 = clock()
+            eng.wait_row(i)                               # this node's mixed rows are back
+            round_stats["wait_s"] += clock() - t0
         data, target = next(node["train-iterator"])
         # gradient averaging keeps .grad as views of the pinned gradient slab: zero in place (the
         # reference's torch 1.7.1 zero_grad behaviour) so backward accumulates into the views
@@ -446,9 +564,27 @@ def next_step(state, params, rundir):
         else:
             node["train-iterator"] = rest
         epoch_done[node["rank"]] = done
+    defer = False
     if not sample:
         if _fused_ok(params):
             fused_round(active, topology, params)         # ★ GPU: gradient + step + mixing
+        elif eng is not None:
+            t0 = clock()
+            eng.wait_all()                                # (every node trained: nothing pending)
+            eng.begin_round()
+            round_stats["wait_s"] += clock() - t0
+            logging.info("  applying own gradient")
+            for i, n in enumerate(active):                # d_sgd.py:51-52, rows sent as they
+                n["optimizer"].step()                     # become final
+                t0 = clock()
+                eng.row_ready(i)
+                round_stats["enqueue_s"] += clock() - t0
+            logging.info("  computing averages of models (GPU, %s, row-streamed)", _mode(params))
+            t0 = clock()
+            eng.mix(_mode(params), False, defer=True)     # ★ GPU
+            round_stats["enqueue_s"] += clock() - t0
+            round_stats["rounds"] += 1
+            defer = True
         else:
             gradient(active, topology, params)
             average(active, topology, params)             # ★ GPU
@@ -460,6 +596,10 @@ def next_step(state, params, rundir):
             n["optimizer"].step()
         sample_average(state["nodes"], active)            # ★ GPU: average + update_models
     state["step"] += 1
+    if defer and not _deferred_ok(params, state, epoch_done, active):
+        t0 = clock()
+        eng.wait_all()                                    # the driver reads models next
+        round_stats["wait_s"] += clock() - t0
     return state, losses, epoch_done, active
 
 
@@ -474,6 +614,10 @@ def main(argv=None):
     ap.add_argument("--unbiased-gradient", action="store_const", const=True, default=False)
     ap.add_argument("--mixing-mode", choices=["exact", "fast"], default="exact",
                     help="exact: bit-identical to the reference loop; fast: clique/MFMA kernels")
+    ap.add_argument("--no-deferred-writeback", dest="deferred_writeback", action="store_false",
+                    help="next_step returns only once every mixed row is back in the models (by "
+                         "default it returns while they stream back, whenever the driver reads no "
+                         "model before the next round: run.py's logging is predicted)")
     args = ap.parse_args(argv)
     rundir = m.rundir(args)
     params = m.params(rundir)
@@ -491,7 +635,7 @@ def main(argv=None):
         "learning-rate": args.learning_rate, "learning-momentum": args.learning_momentum,
         "batch-size": args.batch_size, "initial-averaging": args.initial_averaging,
         "clique-gradient": args.clique_gradient, "unbiased-gradient": args.unbiased_gradient,
-        "mixing-mode": args.mixing_mode,
+        "mixing-mode": args.mixing_mode, "deferred-writeback": args.deferred_writeback,
     })
     if args.rundir is None:
         print(rundir)

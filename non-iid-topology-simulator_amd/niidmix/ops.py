@@ -3,6 +3,9 @@
 Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_csr(x, row_ptr, col, val, out, mode)          k_mix_csr    exact (bit-exact) or fast
   mix_ell(x, ell_col, ell_val, ell_len, out, k, mode)  k_mix_ell  the same, low-degree graphs
+  mix_band(x, ell_col, ell_val, ell_len, out, k, band, mode)
+                                                    k_mix_band   the same, banded rows (a ring in
+                                                    its cycle order, band_layout)
   mix_clique(x, clique_ptr, member_row, member_group, coef, res_ptr, res_col, res_val, res_member,
              row_ptr, col, val, out, max_clique, max_clique_res)
                                                     k_mix_clique (fast, HBM-bound; the CSR is the
@@ -152,6 +155,70 @@ def ell_layout(csr):
     col[r, j] = csr.col
     val[r, j] = csr.val
     return k, col.reshape(-1), val.reshape(-1), lens.astype(np.int32)
+
+
+@torch.library.custom_op("niidmix::mix_band", mutates_args=("out",))
+def mix_band(x: torch.Tensor, ell_col: torch.Tensor, ell_val: torch.Tensor, ell_len: torch.Tensor,
+             out: torch.Tensor, k: int, band: int, mode: int) -> None:
+    """mix_ell over rows whose entries all lie within +-band rows (cyclic; include/niidmix.h
+    niidmix_mix_band_f32).  The band itself is the caller's contract (Mixer checks it once per
+    topology, band_of)."""
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    _req(out.device == x.device, "x and out must be on the same device")
+    n = out.shape[0]
+    _req(x.shape[0] == n, f"x has {x.shape[0]} rows, the band kernel reads exactly the {n} output rows")
+    _vec("ell_col", ell_col, torch.int32, x.device, n * k)
+    _vec("ell_val", ell_val, torch.float32, x.device, n * k)
+    _vec("ell_len", ell_len, torch.int32, x.device, n)
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_band_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n,
+                                       x.shape[1], int(k), int(band), ell_col.data_ptr(),
+                                       ell_val.data_ptr(), ell_len.data_ptr(), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_band")
+
+
+# (ELL width, band) pairs the band kernel is built for
+BAND_OF_K = {3: 1, 5: 2}
+
+
+def band_of(csr, k):
+    """The band B of k_mix_band for this CSR at ELL width k (B = BAND_OF_K[k]) if every entry of row
+    r reads a row r + d (mod N) with |d| <= B, else None.  Needs N >= 2B + 1 and no halo rows."""
+    b = BAND_OF_K.get(k)
+    n = csr.n
+    if b is None or csr.n_in != n or n < 2 * b + 1:
+        return None
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(csr.row_ptr))
+    d = (csr.col.astype(np.int64) - rows) % n
+    return b if bool(np.all((d <= b) | (d >= n - b))) else None
+
+
+def band_layout(csr):
+    """Row order that makes a RING banded (band 1): perm[i] = position of node i along its cycle,
+    starting at node 0 (the reference's ring.create orders nodes by a metric, ring.py:12-27, so the
+    rank order is not the cycle order).  None unless every node has exactly two distinct
+    neighbours, both ways, forming one cycle."""
+    n = csr.n
+    if n < 3 or csr.n_in != n or not np.all(np.diff(csr.row_ptr) == 3):
+        return None
+    nb = csr.col.reshape(n, 3)[:, 1:].astype(np.int64)
+    if np.any(nb[:, 0] == nb[:, 1]) or np.any(nb == np.arange(n)[:, None]):
+        return None
+    order = [0]
+    prev, cur = -1, 0
+    for _ in range(n - 1):
+        a, b = int(nb[cur, 0]), int(nb[cur, 1])
+        nxt = a if a != prev else b
+        if cur not in (int(nb[nxt, 0]), int(nb[nxt, 1])):
+            return None                       # not symmetric
+        prev, cur = cur, nxt
+        order.append(cur)
+    if len(set(order)) != n or 0 not in (int(nb[cur, 0]), int(nb[cur, 1])):
+        return None
+    perm = np.empty(n, np.int64)
+    perm[np.asarray(order, np.int64)] = np.arange(n)
+    return perm
 
 
 @torch.library.custom_op("niidmix::mix_clique", mutates_args=("out",))
@@ -416,7 +483,7 @@ _LAZY = {
     "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
     "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds",
     "w_dense": "dense",
-    "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell",
+    "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell", "band": "ell",
 }
 
 
@@ -598,6 +665,8 @@ class Mixer:
     def _build_ell(self):
         lay = self._hosted("ell", lambda: ell_layout(self.csr))
         self.ell = None if lay is None else lay[0]
+        # the band kernel where the rows are banded as stored (a ring relabeled by band_layout)
+        self.band = None if lay is None else self._hosted("band", lambda: band_of(self.csr, lay[0]))
         if lay is not None:
             k, col, val, ln = lay
             self.e_col = torch.from_numpy(col).to(self.device)
@@ -618,9 +687,11 @@ class Mixer:
                 32 for big cliques
                 (> 256 members, 32-column items: an item is then one contiguous 128 KB stretch;
                 fully-connected 1000 nodes 1.43 vs 1.77 ms).
-        perm is None when the rows are already clique-contiguous."""
+        perm is None when the rows are already clique-contiguous.  Without a clique plan, a ring is
+        put in its cycle order (band_layout: k_mix_band reads it; ring 100 at P = 62 006)."""
         if self.plan is None:
-            return None, memory_block_cols()
+            perm = band_layout(self.csr) if self.ell is not None and self.band is None else None
+            return perm, memory_block_cols()
         order = self.plan.member_row.astype(np.int64)
         perm = np.empty(self.n, np.int64)
         perm[order] = np.arange(self.n)
@@ -681,6 +752,9 @@ class Mixer:
                 return "tile-lds-exact"
             if self.tile is not None:
                 return "tile-exact"
+            if self.band is not None and (x is None or (x.shape[0] == self.n and _lds_ok(x))) \
+                    and (out is None or _lds_ok(out)):
+                return "band-exact"
             return "ell-exact" if self.ell is not None else "csr-exact"
         if self.factored_safe and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
@@ -689,6 +763,9 @@ class Mixer:
         if self.plan is not None and self.tlds is not None and (x is None or _lds_ok(x)) and \
                 (out is None or _lds_ok(out)):
             return "tile-lds-fast"               # clique graph with removed edges
+        if self.band is not None and (x is None or (x.shape[0] == self.n and _lds_ok(x))) \
+                and (out is None or _lds_ok(out)):
+            return "band-fast"
         return "ell-fast" if self.ell is not None else "csr-fast"
 
     def __call__(self, x, out=None, mode="fast", kernel=None):
@@ -704,6 +781,11 @@ class Mixer:
             _req(self.ell is not None, "no ELL layout: a row has more than 8 entries")
             mix_ell(x, self.e_col, self.e_val, self.e_len, out, self.ell,
                     EXACT if k == "ell-exact" else FAST)
+        elif k in ("band-exact", "band-fast"):
+            _req(self.band is not None, "no band layout: rows are not banded as stored "
+                 "(Mixer.device_layout / band_layout gives a ring's cycle order)")
+            mix_band(x, self.e_col, self.e_val, self.e_len, out, self.ell, self.band,
+                     EXACT if k == "band-exact" else FAST)
         elif k in ("tile-exact", "tile-fast"):
             _req(self.tile is not None, f"no tile plan: {self.tile_reason}")
             mix_tile(x, self.t_sub_ptr, self.t_sub_rows, self.t_sub_wself, self.t_pos_src,

@@ -348,3 +348,161 @@ class MultiDeviceRound:
                                 "devices": [str(d) for d in self.devices],
                                 "stripes": self.stripes}
         return hosts[0]
+
+
+# ------------------------------------------------------------------------------------------------
+# row-streamed round: the PCIe copies hidden behind the CPU part of the round
+class ResidentRound:
+    """The host-resident round with its PCIe traffic overlapped with the CPU part of the round
+    (the reference's round is train every node -> optimizer.step() every node
+    -> average, d_sgd.py:186-220).
+
+    The whole slab (each device: its column stripe of every row) stays resident in HBM, in two
+    buffers dx / dy.  Per round:
+      row_ready(i)   node i's parameters are final (right after its optimizer.step(),
+                     d_sgd.py:51-52): once every row of i's block of `block` rows is final, the
+                     block goes H2D on a copy stream while the CPU steps the next nodes;
+      mix(mode)      after the last step: the remaining blocks go up, the kernels mix dx -> dy
+                     (the same Mixer, the same bits as every other path), and dy comes back D2H
+                     block by block in row order, one event per block;
+      wait_row(i)    the next round's training of node i waits only for its own block
+                     (d_sgd.py:186-198 reads row i first in its forward); wait_all() for readers
+                     of every model.
+    Jacobi holds: every H2D of a round precedes its mix (stream order), and the next round's H2D
+    into dx waits for this round's mix.  Several GPUs: one column stripe each, as
+    MultiDeviceRound (bitwise the one-GPU round)."""
+
+    def __init__(self, make_mixer, n, p, devices, block=8, align=1024):
+        from .shard import column_stripe
+        self.n, self.p = n, p
+        self.block = max(1, int(block))
+        self.nblk = -(-n // self.block)
+        self.devices = [torch.device(d) for d in devices]
+        world = len(self.devices)
+        self.parts = []
+        for r, dev in enumerate(self.devices):
+            c0, c1 = column_stripe(p, world, r, align)
+            if c1 <= c0:
+                continue
+            w = c1 - c0
+            part = {"dev": dev, "c0": c0, "w": w, "mixer": make_mixer(dev),
+                    "dx": torch.empty((n, w), dtype=torch.float32, device=dev),
+                    "dy": torch.empty((n, w), dtype=torch.float32, device=dev),
+                    "s_h2d": torch.cuda.Stream(dev), "s_mix": torch.cuda.Stream(dev),
+                    "s_d2h": torch.cuda.Stream(dev), "ev_mix": None}
+            self.parts.append(part)
+        self.host = None
+        self._count = [0] * self.nblk      # rows of each block made final this round
+        self._sent = [False] * self.nblk
+        self._done = None                  # per block: the D2H events of the last mix
+        self.last_timing = None
+
+    @staticmethod
+    def fits(n, p, devices, frac=0.8):
+        """Enough free HBM for the two resident buffers on every device (else: windowed round)."""
+        world = max(1, len(devices))
+        need = 2 * n * (-(-p // world)) * 4
+        for d in devices:
+            free, _ = torch.cuda.mem_get_info(torch.device(d))
+            if need > frac * free:
+                return False
+        return True
+
+    def begin(self, host):
+        """Start a round over `host` (pinned [N, P]): nothing is sent yet."""
+        assert host.shape == (self.n, self.p) and host.dtype == torch.float32 and host.stride(1) == 1
+        self.host = host
+        self._count = [0] * self.nblk
+        self._sent = [False] * self.nblk
+        for pt in self.parts:
+            pt["s_h2d"].wait_stream(pt["s_d2h"])   # the host rows come back before they go up
+
+    def _rows(self, b):
+        r0 = b * self.block
+        return r0, min(self.n, r0 + self.block) - r0
+
+    def _h2d(self, b):
+        r0, rows = self._rows(b)
+        h = self.host
+        ld_h = h.stride(0) * 4
+        for pt in self.parts:
+            s = pt["s_h2d"]
+            if pt["ev_mix"] is not None:
+                s.wait_event(pt["ev_mix"])         # the previous round's mix has read dx
+                pt["ev_mix"] = None
+            _copy2d(pt["dx"].data_ptr() + r0 * pt["w"] * 4, pt["w"] * 4,
+                    h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, ld_h, pt["w"] * 4, rows, 0, s)
+        self._sent[b] = True
+
+    def row_ready(self, i):
+        """Row i of the host slab is final for this round: send its block once it is complete."""
+        if self.host is None:
+            return
+        b = i // self.block
+        self._count[b] += 1
+        if self._count[b] == self._rows(b)[1] and not self._sent[b]:
+            self._h2d(b)
+
+    def mix(self, mode="exact", kernel=None, timing=False):
+        """Enqueue the rest of the round (remaining H2D, mixing, D2H by block); returns at once."""
+        t0 = time.perf_counter()
+        unsent = sum(1 for s in self._sent if not s)
+        for b in range(self.nblk):
+            if not self._sent[b]:
+                self._h2d(b)
+        h = self.host
+        ld_h = h.stride(0) * 4
+        done = [[] for _ in range(self.nblk)]
+        t_ev = []
+        for pt in self.parts:
+            with torch.cuda.device(pt["dev"]):
+                sm, sd = pt["s_mix"], pt["s_d2h"]
+                sm.wait_stream(pt["s_h2d"])
+                sm.wait_stream(sd)                  # dy drained by the previous round's D2H
+                if timing:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(sm)
+                with torch.cuda.stream(sm):
+                    pt["mixer"](pt["dx"], out=pt["dy"], mode=mode, kernel=kernel)
+                ev_mix = torch.cuda.Event()
+                ev_mix.record(sm)
+                pt["ev_mix"] = ev_mix
+                if timing:
+                    ev[1].record(sm)
+                    t_ev.append(ev)
+                sd.wait_event(ev_mix)
+                for b in range(self.nblk):
+                    r0, rows = self._rows(b)
+                    _copy2d(h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, ld_h,
+                            pt["dy"].data_ptr() + r0 * pt["w"] * 4, pt["w"] * 4, pt["w"] * 4,
+                            rows, 1, sd)
+                    e = torch.cuda.Event()
+                    e.record(sd)
+                    done[b].append(e)
+        self._done = done
+        self.host_round = h
+        self.host = None                            # row_ready() is a no-op until begin()
+        self._timing = (timing, t0, t_ev, unsent)
+
+    def wait_row(self, i):
+        """Block until row i's mixed values are back in the host slab."""
+        if self._done is not None:
+            for e in self._done[i // self.block]:
+                e.synchronize()
+
+    def wait_all(self):
+        if self._done is None:
+            return
+        for evs in self._done:
+            for e in evs:
+                e.synchronize()
+        timing, t0, t_ev, unsent = self._timing
+        if timing:
+            self.last_timing = {"mix_to_host_s": time.perf_counter() - t0,
+                                "kernel_ms": [a.elapsed_time(b) for a, b in t_ev],
+                                "blocks_sent_at_mix": unsent, "blocks": self.nblk}
+        self._done = None
+
+    @property
+    def pending(self):
+        return self._done is not None

@@ -1,0 +1,137 @@
+"""k_mix_band (banded rows: a ring in its cycle order) against the reference's own outputs and the
+C oracle: bitwise in exact mode, within the condition-aware tolerance in fast mode, at the float4,
+float2 and scalar paths, both row-group shapes, cyclic wrap on tiny rings, the average-only flag,
+and ring 100 at P = 62 006 inside a hipGraph as bench.py times it."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def _relabeled(csr, dev):
+    from niidmix import ops
+    m = ops.Mixer(csr=csr, device=dev)
+    perm, _ = m.device_layout()
+    if perm is None:                      # already banded as stored (a 3-ring)
+        assert m.band == 1
+        perm = np.arange(csr.n)
+    mr = m.relabeled(perm)
+    assert mr.band == 1
+    return mr, perm
+
+
+@pytest.mark.parametrize("name", ["ring100_p257", "nonfinite_ring8_p16"])
+def test_band_vs_reference_golden(name, gpu, oracle_mod):
+    """The reference's own round (golden y), rows in the ring's cycle order on the device."""
+    from niidmix.topology import MixCSR
+    g = load_golden(name)
+    csr = MixCSR(g["row_ptr"], g["col"], g["val"]).validate()
+    mr, perm = _relabeled(csr, gpu)
+    pt = torch.from_numpy(perm).to(gpu)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    xp = torch.empty_like(x)
+    xp[pt] = x
+    assert mr.kernel_for("exact", xp) == "band-exact" and mr.kernel_for("fast", xp) == "band-fast"
+    y = mr(xp, kernel="band-exact")[pt].cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"])
+    yf = mr(xp, kernel="band-fast")[pt].cpu().numpy()
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(yf, g["y"], bound, rtol=RTOL)
+    assert ok, worst
+
+
+def _ring(n, seed):
+    from niidmix.topology import mh_csr
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(n)
+    edges = {}
+    for i in range(n):
+        a, b = int(order[(i - 1) % n]), int(order[(i + 1) % n])
+        edges[int(order[i])] = [a, b] if rng.random() < 0.5 else [b, a]
+    return mh_csr(n, edges)
+
+
+@pytest.mark.parametrize("rc", ["1,1", "1,2", "1,4", "2,1", "2,2", "4,1", "4,4", "8,2"])
+@pytest.mark.parametrize("n,p", [(3, 1000), (4, 4098), (5, 62006), (17, 1000), (100, 62006),
+                                 (100, 4098), (257, 2048)])
+def test_band_sizes(n, p, rc, gpu, oracle_mod, monkeypatch):
+    from niidmix import ops
+    monkeypatch.setenv("NIIDMIX_BAND_RC", rc)
+    mr, _ = _relabeled(_ring(n, n + p), gpu)
+    c = mr.csr
+    assert mr.kernel_for("exact") == "band-exact"
+    xh = np.random.default_rng(p).standard_normal((n, p)).astype(np.float32)
+    xh[0, 0], xh[n - 1, 1] = np.inf, np.nan
+    x = torch.from_numpy(xh).to(gpu)
+    ref = oracle_mod.mix_exact_c(xh, c.row_ptr, c.col, c.val)
+    assert oracle_mod.bitwise_equal(mr(x, kernel="band-exact").cpu().numpy(), ref)
+    bound = oracle_mod.condition_bound(xh, c.row_ptr, c.col, c.val)
+    ok, worst = oracle_mod.check_tolerance(mr(x, kernel="band-fast").cpu().numpy(), ref, bound,
+                                           rtol=RTOL)
+    assert ok, worst
+    out = torch.empty_like(x)
+    ops.mix_band(x, mr.e_col, mr.e_val, mr.e_len, out, mr.ell, mr.band, ops.EXACT | ops.AVERAGE_ONLY)
+    ref = oracle_mod.mix_exact_c(xh, c.row_ptr, c.col, c.val, average_only=True)
+    assert oracle_mod.bitwise_equal(out.cpu().numpy(), ref)
+
+
+def test_band2_lattice(gpu, oracle_mod):
+    """ELL width 5, band 2 (every node linked to +-1 and +-2, lists in shuffled order); an odd p
+    (scalar rows) falls back to the ELL kernel."""
+    from niidmix import ops
+    from niidmix.topology import mh_csr
+    n, p = 37, 3000
+    rng = np.random.default_rng(1)
+    edges = {i: [int(v) for v in rng.permutation([(i + 1) % n, (i - 1) % n, (i + 2) % n, (i - 2) % n])]
+             for i in range(n)}
+    csr = mh_csr(n, edges)
+    m = ops.Mixer(csr=csr, device=gpu)
+    assert m.band == 2 and m.kernel_for("exact") == "band-exact"
+    xh = rng.standard_normal((n, p)).astype(np.float32)
+    y = m(torch.from_numpy(xh).to(gpu), mode="exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, oracle_mod.mix_exact_c(xh, csr.row_ptr, csr.col, csr.val))
+    xo = torch.from_numpy(xh[:, :2999].copy()).to(gpu)
+    assert m.kernel_for("exact", xo) == "ell-exact"
+    y = m(xo, mode="exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, oracle_mod.mix_exact_c(xh[:, :2999].copy(), csr.row_ptr,
+                                                               csr.col, csr.val))
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_ring100_band_hipgraph(mode, gpu, oracle_mod):
+    """bench.py --config ring100 as timed: cycle-order rows, P = 62 006 (float2 path), the rounds
+    captured in ONE hipGraph (two ping-pong rounds per replay), each round checked against the
+    oracle applied to its own GPU input."""
+    from niidmix import memory
+    from niidmix.topology import MixCSR
+    g = load_golden("ring100_p257")
+    mr, _ = _relabeled(MixCSR(g["row_ptr"], g["col"], g["val"]).validate(), gpu)
+    c = mr.csr
+    p = 62006
+    kernel = mr.kernel_for(mode)
+    assert kernel == "band-" + mode
+    a = memory.empty_slab(100, p, gpu)
+    a.normal_(generator=torch.Generator(device=gpu).manual_seed(2))
+    b = memory.empty_slab(100, p, gpu)
+    mr(a, out=b, kernel=kernel, mode=mode)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        mr(a, out=b, kernel=kernel, mode=mode)
+        mr(b, out=a, kernel=kernel, mode=mode)
+    for _ in range(2):
+        x0 = a.cpu().numpy()
+        graph.replay()
+        torch.cuda.synchronize()
+        y1, y2 = b.cpu().numpy(), a.cpu().numpy()
+        for xin, yout in ((x0, y1), (y1, y2)):
+            ref = oracle_mod.mix_exact_c(xin, c.row_ptr, c.col, c.val)
+            if mode == "exact":
+                assert oracle_mod.bitwise_equal(yout, ref)
+            else:
+                bound = oracle_mod.condition_bound(xin, c.row_ptr, c.col, c.val)
+                ok, worst = oracle_mod.check_tolerance(yout, ref, bound, rtol=RTOL)
+                assert ok, worst

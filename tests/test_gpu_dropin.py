@@ -140,15 +140,16 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
             nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 500:(r + 1) * 500],
                           "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
         topo = {"edges": {0: [1], 1: [0]}, "weights": torch.tensor([[0.5, 0.5], [0.5, 0.5]])}
-        orig = d_sgd.average
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
         if mix == "oracle":
             d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False          # next_step calls gradient + average
         try:
             state, _, _ = d_sgd.init(nodes, topo, params)
             for _ in range(6):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
         finally:
-            d_sgd.average = orig
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
         return [torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone()
                 for n in nodes]
 
@@ -156,6 +157,90 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
     b = run("oracle")
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("resident", ["1", "0"])
+def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypatch):
+    """The row-streamed round (rows go H2D right after their optimizer.step(), the mixed rows come
+    back while the next round trains; niidmix.slab.ResidentRound) with deferred write-back, on a
+    16-node ring of linear MNIST-shaped models over 7 rounds: every round's parameters equal, bit for
+    bit, those of the reference loop doing the mixing (oracle) once synchronised.  next_step really
+    returns early on rounds where run.py reads no model, and returns synchronised on the rounds
+    where run.py's should_log (every 3rd step here) reads them; resident=0 runs the windowed
+    engine (always synchronous)."""
+    from niidmix import d_sgd
+    monkeypatch.setenv("NIIDMIX_RESIDENT", resident)
+    monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")          # ragged last block (16 = 5 x 3 + 1)
+    n = 16
+
+    def run(mix, sync_each=True):
+        torch.manual_seed(1337)
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
+                  "topology": {"name": "ring"},
+                  "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 3,
+                             "log-consensus-distance": False},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 25,
+                                "initial-averaging": False, "clique-gradient": False,
+                                "unbiased-gradient": False, "deferred-writeback": True}}
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc = torch.nn.Linear(784, 10)
+
+            def forward(self, x, params):
+                return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+        g = torch.Generator().manual_seed(7)
+        data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+                for _ in range(n * 200)]
+        nodes = []
+        for r in range(n):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        edges = {r: [(r + 1) % n, (r - 1) % n] if r % 2 else [(r - 1) % n, (r + 1) % n]
+                 for r in range(n)}
+        from niidmix.topology import mh_csr
+        topo = {"edges": edges, "weights": torch.from_numpy(mh_csr(n, edges).dense())}
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False
+        snaps, pend = [], []
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for _ in range(7):
+                state, losses, done, active = d_sgd.next_step(state, params, None)
+                eng = d_sgd._engines.get(id(nodes))
+                pend.append(bool(eng is not None and eng.resident is not None and
+                                 eng.resident.pending))
+                if not sync_each:
+                    continue                   # the next round's training waits row by row
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+            if not sync_each:
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+        return snaps, pend
+
+    a, pend = run("gpu")
+    b, _ = run("oracle")
+    for k, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), k
+    a7, _ = run("gpu", sync_each=False)
+    assert torch.equal(a7[-1], b[-1])
+    if resident == "1":
+        # state['step'] after round k is k + 1: run.py reads models at steps 3 and 6
+        assert pend == [True, True, False, True, True, False, True]
+    else:
+        assert not any(pend)
 
 
 @pytest.mark.parametrize("alg", ["clique", "unbiased"])

@@ -1,0 +1,81 @@
+#!/usr/bin/env python
+"""ring100 (P = 62 006) round time per band-kernel shape (rows x column chunks per wave), the ELL
+kernel and the stream copy of the same slab, each as bench.py times it: K rounds in ONE hipGraph,
+replayed (tuning tool).
+
+    python tools/band_probe.py [--rc 1,1:1,2:2,2:4,4] [--steps 20] [--reps 5]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "non-iid-topology-simulator_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def graph_round_us(step, a, b, steps, reps):
+    step(a, b)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        x, y = a, b
+        for _ in range(steps):
+            step(x, y)
+            x, y = y, x
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3 / steps)
+    return min(ts), float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rc", default="1,1:1,2:1,4:2,1:2,2:4,1:4,4:8,2")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--p", type=int, default=62006)
+    a = ap.parse_args()
+    from bench import golden
+    from niidmix import _lib, memory, ops
+    dev = torch.device("cuda:0")
+    csr, _ = golden("ring100_p257")
+    m = ops.Mixer(csr=csr, device=dev)
+    perm, _ = m.device_layout()
+    mr = m.relabeled(perm)
+    n, p = csr.n, a.p
+    xa = memory.empty_slab(n, p, dev)
+    xa.normal_(generator=torch.Generator(device=dev).manual_seed(1))
+    xb = memory.empty_slab(n, p, dev)
+    print(f"ring {n} x P={p}, {a.steps} rounds per hipGraph replay, min / median of {a.reps} replays")
+    for rc in a.rc.split(":"):
+        os.environ["NIIDMIX_BAND_RC"] = rc
+        us = graph_round_us(lambda x, y: mr(x, out=y, kernel="band-fast"), xa, xb, a.steps, a.reps)
+        print(f"band R,CH={rc:4s}  {us[0]:7.2f} / {us[1]:7.2f} us per round")
+    os.environ.pop("NIIDMIX_BAND_RC", None)
+    for ch in ("1", "2", "4"):
+        os.environ["NIIDMIX_ELL_CH"] = ch
+        us = graph_round_us(lambda x, y: m(x, out=y, kernel="ell-fast"), xa, xb, a.steps, a.reps)
+        print(f"ell CH={ch}         {us[0]:7.2f} / {us[1]:7.2f} us per round (rank order)")
+    os.environ.pop("NIIDMIX_ELL_CH", None)
+    numel = n * p - (n * p) % 4
+    fa, fb = xa.view(-1)[:numel], xb.view(-1)[:numel]
+
+    def cp(x, y):
+        _lib.check(_lib.lib.niidmix_stream_copy_f32(x.data_ptr(), y.data_ptr(), numel,
+                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "copy")
+    us = graph_round_us(cp, fa, fb, a.steps, a.reps)
+    print(f"stream copy       {us[0]:7.2f} / {us[1]:7.2f} us per copy of the slab")
+
+
+if __name__ == "__main__":
+    main()
