@@ -2158,7 +2158,11 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         // the segment walker below.  Position lists: niidmix.tile.build_tile_mfma_positions.
         // Lane l holds D[i = 4 (l >> 4) + r][j = l & 15]: tile row j, parameter columns
         // 8 i + cb (cb: the 8 accumulators), i.e. the 32 consecutive columns 32 (l >> 4) .. +31.
-        if (mf_ptr != nullptr) {
+        // mf_waves >= 0: waves [0, mf_waves) of every block on the matrix cores; mf_waves = -k:
+        // every k-th column chunk's blocks entirely on the matrix cores, the other blocks walk
+        // segments (no matrix-core preamble), so the two pipes are fed by different blocks
+        const bool mf_item = mf_waves >= 0 || chunk % (int64_t)(-mf_waves) == 0;
+        if (mf_ptr != nullptr && mf_item) {
             bool bad = false;
             {
                 const int nf = (grp_src_ptr[grp + 1] - grp_src_ptr[grp]) * (int)CW;
@@ -2187,7 +2191,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 float *srow = lds_tile + slot_j * (int)CW + 32 * g4;
                 // waves [0, mf_waves) take the matrix cores, the others the segment walker: the two
                 // pipes run side by side (a wave on either stores its rows itself)
-                const bool mfw = wave < mf_waves;
+                const bool mfw = wave < (mf_waves >= 0 ? mf_waves : n_waves);
                 const int64_t colw = c0 + 2 * lane;
                 const bool okw = lane < rs && colw < p;
                 const int slw = lane < rs ? lane : rs - 1;

@@ -187,13 +187,16 @@ def _fused_ok(params):
 
 
 class _FusedEngine:
-    """Parameter slab + gradient slab + GradMean + Mixer + FusedRoundRunner (one per GPU stripe
-    when several GPUs are visible, niidmix.slab.MultiDeviceRound)."""
+    """Parameter slab + gradient slab + GradMean + Mixer, run either row-streamed and resident
+    (niidmix.slab.ResidentRound with fused_op: each node's parameter and gradient rows go to the
+    GPU right after its backward(), the mixed parameters and averaged gradients come back while
+    the next round trains) or windowed (FusedRoundRunner); one column stripe per GPU when several
+    are visible (niidmix.slab.MultiDeviceRound)."""
 
     def __init__(self, nodes, topology, params, devices):
         from .gradient import GradMean, build_grad_plan
         from .ops import Mixer
-        from .slab import FusedRoundRunner, MultiDeviceRound, NodeSlab
+        from .slab import FusedRoundRunner, MultiDeviceRound, NodeSlab, ResidentRound, fused_op
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
         self.key = _grad_key(params) + (float(params["algorithm"]["learning-rate"]),)
@@ -207,11 +210,51 @@ class _FusedEngine:
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
         lr = params["algorithm"]["learning-rate"]
 
-        def make(dev, n, cols):
-            mixer = self.mixer if dev == devices[0] else self.mixer.to(dev)
-            return FusedRoundRunner(GradMean(self.plan, dev), self.plan.stepped, lr, mixer, n,
-                                    cols, dev, window=_window())
-        self.runner = MultiDeviceRound(make, self.slab.n, self.slab.p, devices)
+        n, p = self.slab.n, self.slab.p
+        wb = os.environ.get("NIIDMIX_GRAD_WRITEBACK", "1") != "0"
+        self.resident = None
+        self.runner = None
+        if _resident_ok() and ResidentRound.fits(n, p, devices, buffers=4 if wb else 3):
+            self.resident = ResidentRound(
+                lambda dev, part: fused_op(dev, part, GradMean(self.plan, dev), self.plan.stepped,
+                                           lr, self.mixer if dev == devices[0] else self.mixer.to(dev)),
+                n, p, devices, block=_row_block(), n_in=2, n_out=2 if wb else 1)
+            self.outs = (self.slab.host, self.gslab.host) if wb else (self.slab.host,)
+        else:
+            def make(dev, n, cols):
+                mixer = self.mixer if dev == devices[0] else self.mixer.to(dev)
+                return FusedRoundRunner(GradMean(self.plan, dev), self.plan.stepped, lr, mixer, n,
+                                        cols, dev, window=_window())
+            self.runner = MultiDeviceRound(make, n, p, devices)
+
+    # the row-streamed round (resident engine only)
+    def begin_round(self):
+        if self.resident is not None:
+            self.resident.begin(self.slab.host, self.gslab.host, outs=self.outs)
+
+    def row_ready(self, i):
+        if self.resident is not None:
+            self.resident.row_ready(i)
+
+    def wait_row(self, i):
+        if self.resident is not None:
+            self.resident.wait_row(i)
+
+    def wait_all(self):
+        if self.resident is not None:
+            self.resident.wait_all()
+
+    def run(self, mode, timing=False, defer=False):
+        if self.resident is not None:
+            if self.resident.hosts is None:
+                self.begin_round()                    # nothing streamed: every row goes up now
+            self.resident.mix(mode, timing=timing)
+            if not defer:
+                self.resident.wait_all()
+                return self.resident.last_timing
+            return None
+        self.runner.run(self.slab.host, self.gslab.host, mode=mode, timing=timing)
+        return self.runner.last_timing
 
     def valid_for(self, nodes, topology, params):
         models = [n["model"] for n in nodes]
@@ -228,23 +271,38 @@ def fused_round(nodes, topology, params):
     device round: gradient mean, SGD step and mixing on each column window, one H2D of parameters
     and gradients and one D2H of the mixed parameters (niidmix.slab.FusedRoundRunner)."""
     synchronize()
+    eng = _fused_engine(nodes, topology, params)
+    logging.info("  fused gradient %s + SGD step + mixing (GPU, %s)", eng.plan.kind, _mode(params))
+    t = eng.run(_mode(params), timing=logging.getLogger().isEnabledFor(logging.INFO))
+    if t:
+        logging.info("  fused round: %s", t)
+
+
+def _fused_engine(nodes, topology, params):
     key = id(nodes)
     eng = _fused_engines.get(key)
     if eng is None or not eng.valid_for(nodes, topology, params):
+        synchronize()
         eng = _FusedEngine(nodes, topology, params, _devices(nodes))
         _fused_engines.clear()
         _fused_engines[key] = eng
-    logging.info("  fused gradient %s + SGD step + mixing (GPU, %s)", eng.plan.kind, _mode(params))
-    eng.runner.run(eng.slab.host, eng.gslab.host, mode=_mode(params),
-                   timing=logging.getLogger().isEnabledFor(logging.INFO))
-    if eng.runner.last_timing:
-        logging.info("  fused round: %s", eng.runner.last_timing)
+    return eng
 
 
 # ------------------------------------------------------------------------------------------------
 # the GPU mixing step
 def _window():
     return int(os.environ.get("NIIDMIX_WINDOW", 1 << 15))
+
+
+def _resident_ok():
+    """The row-streamed resident rounds (niidmix.slab.ResidentRound); NIIDMIX_RESIDENT=0: the
+    windowed rounds of rounds 1-3."""
+    return os.environ.get("NIIDMIX_RESIDENT", "1") != "0"
+
+
+def _row_block():
+    return int(os.environ.get("NIIDMIX_ROW_BLOCK", 8))
 
 
 class _Engine:
@@ -260,7 +318,7 @@ class _Engine:
 
     def __init__(self, nodes, topology, devices):
         from .ops import Mixer
-        from .slab import MultiDeviceRound, NodeSlab, ResidentRound, SlabMixer
+        from .slab import MultiDeviceRound, NodeSlab, ResidentRound, SlabMixer  # noqa: F401
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
         self.slab = NodeSlab([n["model"] for n in nodes])
@@ -272,10 +330,12 @@ class _Engine:
         n, p = self.slab.n, self.slab.p
         self.resident = None
         self.runner = None
-        if os.environ.get("NIIDMIX_RESIDENT", "1") != "0" and ResidentRound.fits(n, p, devices):
+        if _resident_ok() and ResidentRound.fits(n, p, devices):
+            from .slab import mixing_op
             self.resident = ResidentRound(
-                lambda dev: self.mixer if dev == devices[0] else self.mixer.to(dev), n, p, devices,
-                block=int(os.environ.get("NIIDMIX_ROW_BLOCK", 8)))
+                lambda dev, part: mixing_op(dev, part, self.mixer if dev == devices[0]
+                                            else self.mixer.to(dev)),
+                n, p, devices, block=_row_block())
         else:
             self.runner = MultiDeviceRound(
                 lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
@@ -355,7 +415,7 @@ def synchronize():
     """Wait until the mixed parameters of the last round are all back in the nodes' models.
     next_step may return while they stream back (deferred write-back, _deferred_ok); everything in
     this module that reads or writes the models waits first, and so must any other reader."""
-    for eng in _engines.values():
+    for eng in list(_engines.values()) + list(_fused_engines.values()):
         eng.wait_all()
 
 
@@ -540,14 +600,21 @@ def next_step(state, params, rundir):
     # GPU right after its optimizer.step() and come back while the next round trains
     streamed = not sample and not _averages_gradients(params) and _row_streamed(params)
     eng = _engine(active, topology) if streamed else None
-    if eng is None:
+    # gradient averaging, momentum 0: the fused device round, row-streamed too — each node's
+    # parameter and gradient rows go up right after its backward()
+    feng = (_fused_engine(active, topology, params)
+            if not sample and _fused_ok(params) and _row_streamed(params) else None)
+    if eng is None and feng is None:
         synchronize()
+    if feng is not None:
+        feng.begin_round()
+    weng = eng if eng is not None else feng
     losses, epoch_done = {}, {}
     clock = time.perf_counter
     for i, node in enumerate(active):                     # local training (CPU)
-        if eng is not None:
+        if weng is not None:
             t0 = clock()
-            eng.wait_row(i)                               # this node's mixed rows are back
+            weng.wait_row(i)                              # this node's mixed rows are back
             round_stats["wait_s"] += clock() - t0
         data, target = next(node["train-iterator"])
         # gradient averaging keeps .grad as views of the pinned gradient slab: zero in place (the
@@ -556,6 +623,10 @@ def next_step(state, params, rundir):
         loss = F.nll_loss(node["model"].forward(data, params), target)
         loss.backward()
         losses[node["rank"]] = loss.tolist()
+        if feng is not None:
+            t0 = clock()
+            feng.row_ready(i)                             # its parameters and gradients are final
+            round_stats["enqueue_s"] += clock() - t0
         rest = _peek(node["train-iterator"])
         done = rest is None
         if done:
@@ -566,7 +637,16 @@ def next_step(state, params, rundir):
         epoch_done[node["rank"]] = done
     defer = False
     if not sample:
-        if _fused_ok(params):
+        if feng is not None:
+            t0 = clock()
+            feng.wait_all()
+            logging.info("  fused gradient %s + SGD step + mixing (GPU, %s, row-streamed)",
+                         feng.plan.kind, _mode(params))
+            feng.run(_mode(params), defer=True)           # ★ GPU: gradient + step + mixing
+            round_stats["enqueue_s"] += clock() - t0
+            round_stats["rounds"] += 1
+            eng, defer = feng, True
+        elif _fused_ok(params):
             fused_round(active, topology, params)         # ★ GPU: gradient + step + mixing
         elif eng is not None:
             t0 = clock()

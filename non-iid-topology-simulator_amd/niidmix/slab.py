@@ -357,26 +357,31 @@ class ResidentRound:
     (the reference's round is train every node -> optimizer.step() every node
     -> average, d_sgd.py:186-220).
 
-    The whole slab (each device: its column stripe of every row) stays resident in HBM, in two
-    buffers dx / dy.  Per round:
-      row_ready(i)   node i's parameters are final (right after its optimizer.step(),
-                     d_sgd.py:51-52): once every row of i's block of `block` rows is final, the
-                     block goes H2D on a copy stream while the CPU steps the next nodes;
-      mix(mode)      after the last step: the remaining blocks go up, the kernels mix dx -> dy
-                     (the same Mixer, the same bits as every other path), and dy comes back D2H
-                     block by block in row order, one event per block;
+    The host slabs (each device: its column stripe of every row) stay resident in HBM: `n_in`
+    input buffers (the parameter slab; with gradient averaging also the gradient slab) and `n_out`
+    output buffers.  Per round:
+      row_ready(i)   node i's rows are final (its parameters right after its optimizer.step(),
+                     d_sgd.py:51-52; its gradients right after its backward(), d_sgd.py:196):
+                     once every row of i's block of `block` rows is final, the block goes H2D on
+                     a copy stream while the CPU carries on with the next nodes;
+      mix(mode)      after the last node: the remaining blocks go up, the device op runs (for the
+                     plain round the Mixer: dx -> dy, the same bits as every other path), and the
+                     outputs come back D2H block by block in row order, one event per block;
       wait_row(i)    the next round's training of node i waits only for its own block
-                     (d_sgd.py:186-198 reads row i first in its forward); wait_all() for readers
-                     of every model.
-    Jacobi holds: every H2D of a round precedes its mix (stream order), and the next round's H2D
-    into dx waits for this round's mix.  Several GPUs: one column stripe each, as
-    MultiDeviceRound (bitwise the one-GPU round)."""
+                     (d_sgd.py:186-198 reads row i first); wait_all() for readers of every model.
+    Jacobi holds: every H2D of a round precedes its op (stream order), and the next round's H2D
+    into the inputs waits for this round's op.  Several GPUs: one column stripe each, as
+    MultiDeviceRound (bitwise the one-GPU round).
 
-    def __init__(self, make_mixer, n, p, devices, block=8, align=1024):
+      make_op(dev, part) -> op(ins, outs, mode, kernel)   the device op of one stripe
+                            (part: the stripe's dict; ops may keep state in it)"""
+
+    def __init__(self, make_op, n, p, devices, block=8, align=1024, n_in=1, n_out=1):
         from .shard import column_stripe
         self.n, self.p = n, p
         self.block = max(1, int(block))
         self.nblk = -(-n // self.block)
+        self.n_in, self.n_out = n_in, n_out
         self.devices = [torch.device(d) for d in devices]
         world = len(self.devices)
         self.parts = []
@@ -385,33 +390,44 @@ class ResidentRound:
             if c1 <= c0:
                 continue
             w = c1 - c0
-            part = {"dev": dev, "c0": c0, "w": w, "mixer": make_mixer(dev),
-                    "dx": torch.empty((n, w), dtype=torch.float32, device=dev),
-                    "dy": torch.empty((n, w), dtype=torch.float32, device=dev),
+            mk = lambda: torch.empty((n, w), dtype=torch.float32, device=dev)  # noqa: E731
+            part = {"dev": dev, "c0": c0, "w": w,
+                    "ins": [mk() for _ in range(n_in)], "outs": [mk() for _ in range(n_out)],
                     "s_h2d": torch.cuda.Stream(dev), "s_mix": torch.cuda.Stream(dev),
                     "s_d2h": torch.cuda.Stream(dev), "ev_mix": None}
+            part["op"] = make_op(dev, part)
             self.parts.append(part)
-        self.host = None
+        self.hosts = None
+        self.hosts_out = None
         self._count = [0] * self.nblk      # rows of each block made final this round
         self._sent = [False] * self.nblk
-        self._done = None                  # per block: the D2H events of the last mix
+        self._done = None                  # per block: the D2H events of the last op
         self.last_timing = None
 
     @staticmethod
-    def fits(n, p, devices, frac=0.8):
-        """Enough free HBM for the two resident buffers on every device (else: windowed round)."""
+    def fits(n, p, devices, buffers=2, frac=0.8):
+        """Enough free HBM for the resident buffers on every device (else: windowed round)."""
         world = max(1, len(devices))
-        need = 2 * n * (-(-p // world)) * 4
+        need = buffers * n * (-(-p // world)) * 4
         for d in devices:
             free, _ = torch.cuda.mem_get_info(torch.device(d))
             if need > frac * free:
                 return False
         return True
 
-    def begin(self, host):
-        """Start a round over `host` (pinned [N, P]): nothing is sent yet."""
-        assert host.shape == (self.n, self.p) and host.dtype == torch.float32 and host.stride(1) == 1
-        self.host = host
+    @property
+    def host(self):
+        return None if self.hosts is None else self.hosts[0]
+
+    def begin(self, *hosts, outs=None):
+        """Start a round: `hosts` are the pinned [N, P] input slabs (n_in of them), `outs` the host
+        slabs the outputs return to (default: the first n_out inputs).  Nothing is sent yet."""
+        assert len(hosts) == self.n_in
+        for h in hosts:
+            assert h.shape == (self.n, self.p) and h.dtype == torch.float32 and h.stride(1) == 1
+        self.hosts = list(hosts)
+        self.hosts_out = list(outs) if outs is not None else list(hosts[:self.n_out])
+        assert len(self.hosts_out) == self.n_out
         self._count = [0] * self.nblk
         self._sent = [False] * self.nblk
         for pt in self.parts:
@@ -423,20 +439,21 @@ class ResidentRound:
 
     def _h2d(self, b):
         r0, rows = self._rows(b)
-        h = self.host
-        ld_h = h.stride(0) * 4
         for pt in self.parts:
             s = pt["s_h2d"]
             if pt["ev_mix"] is not None:
-                s.wait_event(pt["ev_mix"])         # the previous round's mix has read dx
+                s.wait_event(pt["ev_mix"])         # the previous round's op has read the inputs
                 pt["ev_mix"] = None
-            _copy2d(pt["dx"].data_ptr() + r0 * pt["w"] * 4, pt["w"] * 4,
-                    h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, ld_h, pt["w"] * 4, rows, 0, s)
+            w = pt["w"]
+            for h, d in zip(self.hosts, pt["ins"]):
+                _copy2d(d.data_ptr() + r0 * w * 4, w * 4,
+                        h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4, w * 4,
+                        rows, 0, s)
         self._sent[b] = True
 
     def row_ready(self, i):
-        """Row i of the host slab is final for this round: send its block once it is complete."""
-        if self.host is None:
+        """Row i of the input slabs is final for this round: send its block once it is complete."""
+        if self.hosts is None:
             return
         b = i // self.block
         self._count[b] += 1
@@ -444,26 +461,25 @@ class ResidentRound:
             self._h2d(b)
 
     def mix(self, mode="exact", kernel=None, timing=False):
-        """Enqueue the rest of the round (remaining H2D, mixing, D2H by block); returns at once."""
+        """Enqueue the rest of the round (remaining H2D, the device op, D2H by block); returns at
+        once."""
         t0 = time.perf_counter()
         unsent = sum(1 for s in self._sent if not s)
         for b in range(self.nblk):
             if not self._sent[b]:
                 self._h2d(b)
-        h = self.host
-        ld_h = h.stride(0) * 4
         done = [[] for _ in range(self.nblk)]
         t_ev = []
         for pt in self.parts:
             with torch.cuda.device(pt["dev"]):
                 sm, sd = pt["s_mix"], pt["s_d2h"]
                 sm.wait_stream(pt["s_h2d"])
-                sm.wait_stream(sd)                  # dy drained by the previous round's D2H
+                sm.wait_stream(sd)                  # outputs drained by the previous round's D2H
                 if timing:
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     ev[0].record(sm)
                 with torch.cuda.stream(sm):
-                    pt["mixer"](pt["dx"], out=pt["dy"], mode=mode, kernel=kernel)
+                    pt["op"](pt["ins"], pt["outs"], mode, kernel)
                 ev_mix = torch.cuda.Event()
                 ev_mix.record(sm)
                 pt["ev_mix"] = ev_mix
@@ -471,21 +487,21 @@ class ResidentRound:
                     ev[1].record(sm)
                     t_ev.append(ev)
                 sd.wait_event(ev_mix)
+                w = pt["w"]
                 for b in range(self.nblk):
                     r0, rows = self._rows(b)
-                    _copy2d(h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, ld_h,
-                            pt["dy"].data_ptr() + r0 * pt["w"] * 4, pt["w"] * 4, pt["w"] * 4,
-                            rows, 1, sd)
+                    for h, d in zip(self.hosts_out, pt["outs"]):
+                        _copy2d(h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4,
+                                d.data_ptr() + r0 * w * 4, w * 4, w * 4, rows, 1, sd)
                     e = torch.cuda.Event()
                     e.record(sd)
                     done[b].append(e)
         self._done = done
-        self.host_round = h
-        self.host = None                            # row_ready() is a no-op until begin()
+        self.hosts = None                           # row_ready() is a no-op until begin()
         self._timing = (timing, t0, t_ev, unsent)
 
     def wait_row(self, i):
-        """Block until row i's mixed values are back in the host slab."""
+        """Block until row i's outputs are back in the host slabs."""
         if self._done is not None:
             for e in self._done[i // self.block]:
                 e.synchronize()
@@ -498,7 +514,7 @@ class ResidentRound:
                 e.synchronize()
         timing, t0, t_ev, unsent = self._timing
         if timing:
-            self.last_timing = {"mix_to_host_s": time.perf_counter() - t0,
+            self.last_timing = {"op_to_host_s": time.perf_counter() - t0,
                                 "kernel_ms": [a.elapsed_time(b) for a, b in t_ev],
                                 "blocks_sent_at_mix": unsent, "blocks": self.nblk}
         self._done = None
@@ -506,3 +522,37 @@ class ResidentRound:
     @property
     def pending(self):
         return self._done is not None
+
+
+def mixing_op(dev, part, mixer):
+    """ResidentRound device op of the plain round: Θ' = Wᵀ Θ with the stripe's Mixer (kept in
+    part['mixer'], replaced on a new topology)."""
+    part["mixer"] = mixer
+
+    def op(ins, outs, mode, kernel):
+        part["mixer"](ins[0], out=outs[0], mode=mode, kernel=kernel)
+    return op
+
+
+def fused_op(dev, part, grad_op, step_rows, lr, mixer, grad_writeback=True):
+    """ResidentRound device op of the round with gradient averaging (FusedRoundRunner's per-window
+    arithmetic on the whole stripe): ins = [params, grads] -> averaged gradients (outs[1]) -> SGD
+    step of the stepped rows on the parameters in place -> mixing into outs[0]."""
+    from . import ops
+    part["mixer"] = mixer
+    rows = torch.as_tensor(step_rows, dtype=torch.int32).to(dev)
+    neg_lr = -float(lr)
+
+    def op(ins, outs, mode, kernel):
+        xp, xg = ins
+        if len(outs) > 1:
+            gm = outs[1]
+        else:                                 # no write-back of the averaged gradients
+            if "dm" not in part:
+                part["dm"] = torch.empty_like(xg)
+            gm = part["dm"]
+        grad_op(xg, out=gm)
+        if rows.numel():
+            ops.sgd_step_rows(xp, gm, rows, neg_lr)
+        part["mixer"](xp, out=outs[0], mode=mode, kernel=kernel)
+    return op

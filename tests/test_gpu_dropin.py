@@ -267,13 +267,17 @@ def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
             nds[r]["optimizer"].step()
 
     def run(path):
-        monkeypatch.setenv("NIIDMIX_FUSED", "1" if path == "fused" else "0")
+        monkeypatch.setenv("NIIDMIX_FUSED", "1" if path.startswith("fused") else "0")
+        monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")      # blocks of 3 rows: a ragged last block
         torch.manual_seed(1337)
         params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
                   "topology": {"name": "d-cliques", "remove-clique-edges": 0},
+                  "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 0,
+                             "log-consensus-distance": False},
                   "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 50,
                                 "initial-averaging": False, "clique-gradient": alg == "clique",
-                                "unbiased-gradient": alg == "unbiased"}}
+                                "unbiased-gradient": alg == "unbiased",
+                                "deferred-writeback": path == "fused_deferred"}}
 
         class Net(torch.nn.Module):
             def __init__(self):
@@ -302,20 +306,31 @@ def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
             d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
         try:
             state, _, _ = d_sgd.init(nodes, topo, params)
+            pend = []
             for _ in range(5):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
+                eng = d_sgd._fused_engines.get(id(nodes))
+                pend.append(bool(eng is not None and eng.resident is not None and
+                                 eng.resident.pending))
+            d_sgd.synchronize()
         finally:
             d_sgd.gradient, d_sgd.average = orig_g, orig_a
+        if path == "fused_deferred":
+            assert all(pend), pend                 # next_step returned before the write-back
+        elif path == "fused":
+            assert not any(pend), pend
         return [(torch.cat([q.detach().reshape(-1) for q in n["model"].parameters()]).clone(),
                  torch.cat([q.grad.detach().reshape(-1) for q in n["model"].parameters()]).clone())
                 for n in nodes]
 
     fused, unfused, ref = run("fused"), run("unfused"), run("oracle")
-    for u, v, r in zip(fused, unfused, ref):
+    deferred = run("fused_deferred")
+    for u, v, r, d in zip(fused, unfused, ref, deferred):
         assert torch.equal(v[0], r[0]) and torch.equal(v[1], r[1])
         assert torch.equal(u[0], r[0])
         # the fused round writes the averaged gradients back where the reference leaves them
         assert torch.equal(u[1], r[1])
+        assert torch.equal(d[0], r[0]) and torch.equal(d[1], r[1])
 
 
 def test_sgd_step_rows_matches_torch_cpu_sgd(gpu):

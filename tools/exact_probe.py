@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--order", default="clique", choices=["rank", "clique"])
     ap.add_argument("--no-check", action="store_true", help="phase-split builds: results are not the mix")
+    ap.add_argument("--mf-items", default="",
+                    help="comma list of k: also time the matrix-core path on every k-th column "
+                         "chunk (NIIDMIX_TLDS_MF_WAVES=-k), the segment walker on the others")
+    ap.add_argument("--metas", default="mfma,seg,pos", help="RT 16 variants to time")
     ap.add_argument("--lds-rows", type=int, default=0,
                     help="occupancy probe: reserve LDS for this many staged rows (max_src) per block")
     a = ap.parse_args()
@@ -56,9 +60,14 @@ def main():
     res = {}
     for rep in range(a.reps):
         for rt, m in mixers.items():
-            for meta in (("mfma", "seg", "pos") if rt == 16 else ("pos",)):
-                m.use_segments = meta in ("seg", "mfma")
-                m.use_mfma = meta == "mfma"
+            metas = a.metas.split(",") + [f"mfitem{k}" for k in a.mf_items.split(",") if k]
+            for meta in (metas if rt == 16 else ("pos",)):
+                m.use_segments = meta != "pos"
+                m.use_mfma = meta.startswith("mf")
+                if meta.startswith("mfitem"):
+                    os.environ["NIIDMIX_TLDS_MF_WAVES"] = "-" + meta[6:]
+                else:
+                    os.environ.pop("NIIDMIX_TLDS_MF_WAVES", None)
                 m(x, out=y, kernel="tile-lds-exact")
                 torch.cuda.synchronize()
                 if ref is None:
