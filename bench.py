@@ -278,15 +278,19 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
 def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
     """The drop-in's whole round, d_sgd.next_step (d_sgd.py:178-254) on the same topology: N nodes
     training on the CPU (synthetic data, a Linear(1023, 1024) model = 2^20 fp32 parameters, batch
-    16), each node's optimizer.step(), then the mixing.  Variants, each timed over `rounds` rounds
-    after one warm-up round (median per round):
-      cpu_only        the same rounds with the mixing removed (the CPU part of the round);
-      row_streamed    the plugin's default: rows go H2D right after their optimizer.step(), the
-                      mixed rows come back while the next round trains (deferred write-back);
+    16), each node's optimizer.step(), then the mixing.  Variants, all built first and then run
+    round-robin (round k of every variant before round k + 1 of any, so that drifts of the host's
+    speed hit all of them alike), each timed over `rounds` rounds after one warm-up round:
+      cpu_only            the same rounds with the mixing removed (the CPU part of the round);
+      row_streamed        the plugin's default: rows go H2D right after their optimizer.step(),
+                          the mixed rows come back while the next round trains (deferred write-back);
       row_streamed_sync   the same, but next_step waits for every mixed row before returning;
-      windowed        the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0).
-    exposed_ms = round - cpu_only (the mixing's cost the round still pays); host_blocked_ms = the
-    time next_step itself spent waiting for rows or enqueueing copies and kernels (d_sgd.round_stats)."""
+      windowed            the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0);
+      fused_*             the same two with --clique-gradient (gradient mean + SGD step + mixing
+                          on the device; parameter and gradient rows go up after each backward).
+    exposed_ms = median round - median cpu_only round (the mixing's cost the round still pays);
+    host_blocked_ms = the time next_step itself spent waiting for rows or enqueueing copies and
+    kernels (d_sgd.round_stats), the part of exposed_ms the plugin controls."""
     from niidmix import d_sgd
     n = csr.n
     edges = csr.edges()
@@ -306,66 +310,79 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         def forward(self, x, params):
             return torch.nn.functional.log_softmax(self.fc(x), dim=1)
 
-    def run(variant):
-        env_old = {k: os.environ.get(k) for k in ("NIIDMIX_RESIDENT",)}
-        if variant == "windowed":
-            os.environ["NIIDMIX_RESIDENT"] = "0"
+    variants = ["cpu_only", "row_streamed", "row_streamed_sync", "windowed"]
+    if cliques:
+        variants += ["fused_row_streamed", "fused_windowed"]
+    orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+    env_res = os.environ.get("NIIDMIX_RESIDENT")
+
+    def make(v):
+        fused = v.startswith("fused")
         params = {"meta": {"log": "WARNING", "seed": 1337}, "topology": {"name": "d-cliques"},
                   "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 0,
                              "log-consensus-distance": False},
                   "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": batch,
-                                "initial-averaging": False, "clique-gradient": False,
+                                "initial-averaging": False, "clique-gradient": fused,
                                 "unbiased-gradient": False, "mixing-mode": mode,
-                                "deferred-writeback": variant == "row_streamed"}}
+                                "deferred-writeback": v in ("row_streamed", "fused_row_streamed")}}
         torch.manual_seed(3)
         nodes = []
         for r in range(n):
             mdl = Net()
             nodes.append({"rank": r, "epoch": 0, "train-set": data, "model": mdl,
                           "optimizer": d_sgd.optimizer(mdl, params)})
-        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
-        if variant == "cpu_only":
+        return {"params": params, "nodes": nodes, "ts": [], "blocked": 0.0, "wait": 0.0}
+
+    def step(v, st, k):
+        if v == "cpu_only":
             d_sgd.average = lambda nds, t, p: None
             d_sgd._row_streamed = lambda p: False
-        ts = []
+        if v.endswith("windowed"):
+            os.environ["NIIDMIX_RESIDENT"] = "0"          # read when the engine is built
         try:
-            state, _, _ = d_sgd.init(nodes, topo, params)
-            for k in range(rounds + 1):
-                if k == 1:
-                    for key in d_sgd.round_stats:
-                        d_sgd.round_stats[key] = 0
-                t0 = time.perf_counter()
-                state, _, _, _ = d_sgd.next_step(state, params, None)
-                ts.append(time.perf_counter() - t0)
-            d_sgd.synchronize()
-            st = dict(d_sgd.round_stats)
+            for key in ("wait_s", "enqueue_s"):
+                d_sgd.round_stats[key] = 0.0
+            t0 = time.perf_counter()
+            if k < 0:
+                st["state"], _, _ = d_sgd.init(st["nodes"], topo, st["params"])
+            else:
+                st["state"], _, _, _ = d_sgd.next_step(st["state"], st["params"], None)
+            dt = time.perf_counter() - t0
+            if k >= 1:
+                st["ts"].append(dt)
+                st["blocked"] += d_sgd.round_stats["wait_s"] + d_sgd.round_stats["enqueue_s"]
+                st["wait"] += d_sgd.round_stats["wait_s"]
         finally:
             d_sgd.average, d_sgd._row_streamed = orig, orig_rs
-            for k, v in env_old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-            d_sgd._engines.clear()
-        del nodes, state
-        torch.cuda.empty_cache()
-        t = float(np.median(ts[1:]))
-        out = {"round_ms": round(t * 1e3, 1), "round_ms_min": round(min(ts[1:]) * 1e3, 1)}
-        if variant.startswith("row_streamed") and st["rounds"]:
-            out["host_blocked_ms"] = round((st["wait_s"] + st["enqueue_s"]) / rounds * 1e3, 2)
-            out["host_wait_ms"] = round(st["wait_s"] / rounds * 1e3, 2)
-        return out
+            if env_res is None:
+                os.environ.pop("NIIDMIX_RESIDENT", None)
+            else:
+                os.environ["NIIDMIX_RESIDENT"] = env_res
 
+    d_sgd.MAX_ENGINES = max(d_sgd.MAX_ENGINES, len(variants))
+    sts = {v: make(v) for v in variants}
+    for k in range(-1, rounds + 1):                     # init, one warm-up round, timed rounds
+        for v in variants:
+            step(v, sts[v], k)
+        print(f"[bench --e2e-step] round {k} done", file=sys.stderr, flush=True)
+    d_sgd.synchronize()
     res = {"nodes": n, "p": in_f * out_f + out_f, "model": f"Linear({in_f}, {out_f})",
-           "batch": batch, "rounds_timed": rounds, "mode": mode, "threads": torch.get_num_threads()}
-    for v in ("cpu_only", "row_streamed", "row_streamed_sync", "windowed", "cpu_only"):
-        r = run(v)
-        print(f"[bench --e2e-step] {v}: {r}", file=sys.stderr, flush=True)
-        key = v if v not in res else v + "_again"
-        res[key] = r
-    base = min(res["cpu_only"]["round_ms"], res["cpu_only_again"]["round_ms"])
-    for v in ("row_streamed", "row_streamed_sync", "windowed"):
-        res[v]["exposed_ms"] = round(res[v]["round_ms"] - base, 1)
+           "batch": batch, "rounds_timed": rounds, "mode": mode, "threads": torch.get_num_threads(),
+           "order": "round-robin over the variants"}
+    base = float(np.median(sts["cpu_only"]["ts"]))
+    for v in variants:
+        st = sts[v]
+        out = {"round_ms": round(float(np.median(st["ts"])) * 1e3, 1),
+               "round_ms_min": round(min(st["ts"]) * 1e3, 1)}
+        if v != "cpu_only":
+            out["exposed_ms"] = round((float(np.median(st["ts"])) - base) * 1e3, 1)
+            out["host_blocked_ms"] = round(st["blocked"] / rounds * 1e3, 2)
+            out["host_wait_ms"] = round(st["wait"] / rounds * 1e3, 2)
+        res[v] = out
+    d_sgd._engines.clear()
+    d_sgd._fused_engines.clear()
+    del sts
+    torch.cuda.empty_cache()
     return res
 
 

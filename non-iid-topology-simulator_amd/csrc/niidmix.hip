@@ -833,12 +833,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     const int wave = wave_id();
     const int lane = threadIdx.x & (kWave - 1);
     const int q = lane / LQ, lc = lane - q * LQ;
-    const int64_t t = blockIdx.x;
-    if (t >= n_items) return;
+    // one item per block, or (a grid of fewer blocks, a multiple of 8) items t, t + gridDim, ...:
+    // then each XCD has only gridDim / 8 consecutive items of its sequence in flight, so the
+    // column chunks they span (and the gateway rows they gather) stay within its L2
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
     const int64_t local = t >> 3;
     const int64_t chunk = (local / n_cg) * 8 + (t & 7);
     const int64_t cg = local % n_cg;
-    if (chunk * CW >= p) return;               // block-uniform, before any barrier
+    if (chunk * CW >= p) continue;             // block-uniform, before any barrier
     const bool act = chunk * CW + 4 * lc < p;  // p % 4 == 0: a lane's 4 columns are all in or out
     const unsigned lo = act ? (unsigned)(4 * lc) : 0u;
     const int64_t kb = chunk >> cpb_shift, cin = chunk - (kb << cpb_shift);
@@ -1002,6 +1004,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
                 stv_nt<4>(yc + row * ld_y + lo, o);
             }
         }
+    }
+    if (t + (int64_t)gridDim.x < n_items) __syncthreads();   // red / tot are rewritten next item
     }
 }
 
@@ -2832,7 +2836,16 @@ int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
     // 32-bit row offsets when every block (column-blocked slabs) spans < 4 GiB
     const bool off32 = bg.bc_shift < 62 && bg.bs_x * 4 <= (int64_t)0xffffffffLL &&
                        bg.bs_y * 4 <= (int64_t)0xffffffffLL;
-#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)n_items), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
+    // NIIDMIX_Q_PERSIST=k (tuning): k blocks per CU loop over the items instead of one block each
+    int64_t grid = n_items;
+    if (const char *e = getenv("NIIDMIX_Q_PERSIST")) {
+        const int k = atoi(e);
+        int dev = 0, n_cu = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
+        if (k > 0 && (int64_t)k * n_cu < n_items) grid = (int64_t)k * n_cu / 8 * 8;
+    }
+#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)grid), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
     if (off32) NIIDMIX_CQ(true); else NIIDMIX_CQ(false);
 #undef NIIDMIX_CQ
     return check_launch("k_mix_clique_q");
@@ -3291,8 +3304,9 @@ int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
                  : (p % 2 == 0 && ld_x % 2 == 0 && ld_y % 2 == 0 && (align & 7) == 0) ? 2 : 1;
     if (vw == 1) return set_error(NIIDMIX_EUNSUPPORTED, "band kernel needs even p and ld, 8-B aligned slabs");
     // rows per wave x column chunks per wave (R x CH): NIIDMIX_BAND_RC = "R,CH" among the built
-    // shapes (tuning); default 4 x 4
-    int rr = 4, ch = 4;
+    // shapes (tuning); default 4 x 1 (ring 100, P = 62 006 in a hipGraph: 15.6 us per round; 4 x 4
+    // 18.3, 2 x 2 15.8, 1 x 4 16.5, 8 x 2 17.3; tools/band_probe.py, profiles/r04/band_probe.txt)
+    int rr = 4, ch = 1;
     if (const char *e = getenv("NIIDMIX_BAND_RC")) {
         int a = 0, b = 0;
         if (sscanf(e, "%d,%d", &a, &b) == 2 &&

@@ -284,8 +284,10 @@ def _fused_engine(nodes, topology, params):
     if eng is None or not eng.valid_for(nodes, topology, params):
         synchronize()
         eng = _FusedEngine(nodes, topology, params, _devices(nodes))
-        _fused_engines.clear()
+        _fused_engines.pop(key, None)
         _fused_engines[key] = eng
+        while len(_fused_engines) > MAX_ENGINES:
+            _fused_engines.pop(next(iter(_fused_engines)))
     return eng
 
 
@@ -402,6 +404,8 @@ class _Engine:
 
 
 _engines = {}
+# engines (pinned slab + device buffers) kept per node list, the most recent ones
+MAX_ENGINES = int(os.environ.get("NIIDMIX_MAX_ENGINES", 4))
 
 
 def _mode(params):
@@ -427,8 +431,10 @@ def _engine(nodes, topology):
     if eng is None or not eng.valid_for(nodes, topology):
         synchronize()
         eng = _Engine(nodes, topology, _devices(nodes))
-        _engines.clear()
+        _engines.pop(key, None)
         _engines[key] = eng
+        while len(_engines) > MAX_ENGINES:               # oldest node lists first
+            _engines.pop(next(iter(_engines)))
     return eng
 
 

@@ -585,7 +585,9 @@ def test_multi_clique_tile_auto(n, inter, size, gpu, oracle_mod, monkeypatch):
     y1 = m(x, kernel="clique").cpu().numpy()
     ok, worst = oracle_mod.check_tolerance(y1, ref, bound, rtol=RTOL)
     assert ok, worst
-    assert not np.array_equal(y, y1) or n < 4096    # the two tiles really differ (summation order)
+    # the 8 x 13 multi-clique tile sums in another order than the one-clique 16 x 7 tile; for
+    # 105-112 members both are 16 waves x 7 rows, so the group sums come out bit-identical
+    assert not np.array_equal(y, y1) or n < 4096 or size > 104
     monkeypatch.delenv("NIIDMIX_CLIQUE_Q")
     perm, bc = m.device_layout()
     mr = m.relabeled(perm)
