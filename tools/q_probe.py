@@ -89,8 +89,9 @@ def main():
         for v, ts in times.items():
             if ts:
                 t = min(ts)
+                gbs = alg / (t / 1e3) / 1e9                       # t in ms
                 print(f"SUMMARY n={a.n} B={bc} {v}: min {t:.3f} ms mean {np.mean(ts):.3f} ms "
-                      f"= {alg / t / 1e9:.0f} GB/s = {alg / t / 1e9 / 8000:.3f} of 8 TB/s", flush=True)
+                      f"= {gbs:.0f} GB/s = {gbs / 8000:.3f} of 8 TB/s", flush=True)
         del xb, yb
         torch.cuda.empty_cache()
 

@@ -31,4 +31,7 @@ if g("SQ_INSTS_VALU") and g("SQ_WAVES"):
 if g("SQ_INSTS_MFMA") and g("SQ_WAVES"):
     print(f"MFMA instructions per wave {g('SQ_INSTS_MFMA') / g('SQ_WAVES'):.0f}")
 if g("SQ_VALU_MFMA_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
-    print(f"SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 256 CUs) = {g('SQ_VALU_MFMA_BUSY_CYCLES') / (g('GRBM_GUI_ACTIVE') * 256):.3f}")
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs; the MFMA busy cycles are per-SIMD cycles summed
+    # over the 1024 SIMDs (MI355X_MICROARCH.md): busy / (GRBM / 8 x 1024)
+    print(f"MFMA pipe busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) = "
+          f"{g('SQ_VALU_MFMA_BUSY_CYCLES') / (g('GRBM_GUI_ACTIVE') / 8 * 1024):.3f}")
