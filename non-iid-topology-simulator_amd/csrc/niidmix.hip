@@ -2236,29 +2236,69 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
 #pragma unroll
                         for (int cb = 0; cb < 8; ++cb) acc[cb][r] = xs[cb] * 0.f + ws_j * xs[cb];
                     }
+                    // Positions in groups of 4 (one 16x16x4 MFMA k-block per column block),
+                    // software-pipelined: the descriptors (slot, weight, row mask) of group q + 1
+                    // come by ds_bpermute and its rows by ds_read while group q's products and
+                    // MFMAs issue, and the descriptor words of the next 64 positions are loaded
+                    // one chunk ahead (round 3 waited for both at every group: ~45 % of a
+                    // group's 256 MFMA cycles, profiles/r04/exact_mfma_pipelined.txt)
                     const int e0 = mf_ptr[sub], e1 = mf_ptr[sub + 1];
-                    for (int eb = e0; eb < e1; eb += 64) {
-                        const int cnt = e1 - eb < 64 ? e1 - eb : 64;           // a multiple of 4
-                        const int4 d = reinterpret_cast<const int4 *>(mf)[eb + (lane < cnt ? lane : cnt - 1)];
-                        for (int q = 0; q < cnt; q += 4) {
-                            if (NIIDMIX_MF_SPLIT == 3) break;                 // tuning builds only
-                            const int src = q + g4;                           // position q + k, k = l >> 4
-                            const int slot = __shfl(d.x, src);
-                            const float w = __int_as_float(__shfl(d.y, src));
-                            const uint32_t m = (uint32_t)__shfl(d.z, src);
-                            const float bv = ((m >> jr) & 1u) ? 1.f : 0.f;
-                            const float *xr = lds_tile + slot * (int)CW + 8 * jr;
-                            const float4 x0 = *reinterpret_cast<const float4 *>(xr);
-                            const float4 x1 = *reinterpret_cast<const float4 *>(xr + 4);
-                            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.x, bv, acc[0], 0, 0, 0);
-                            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.y, bv, acc[1], 0, 0, 0);
-                            acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.z, bv, acc[2], 0, 0, 0);
-                            acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x0.w, bv, acc[3], 0, 0, 0);
-                            acc[4] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.x, bv, acc[4], 0, 0, 0);
-                            acc[5] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.y, bv, acc[5], 0, 0, 0);
-                            acc[6] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.z, bv, acc[6], 0, 0, 0);
-                            acc[7] = __builtin_amdgcn_mfma_f32_16x16x4f32(w * x1.w, bv, acc[7], 0, 0, 0);
+                    const int npos = e1 - e0;                                  // a multiple of 4
+                    auto ldd = [&](int off) {                                  // 64 positions' words
+                        const int cnt = npos - off < 64 ? npos - off : 64;
+                        return reinterpret_cast<const int4 *>(mf)[e0 + off + (lane < cnt ? lane : cnt - 1)];
+                    };
+                    int4 dc = ldd(0);
+                    int4 dn = npos > 64 ? ldd(64) : dc;
+                    auto desc = [&](const int4 &d, int q, int &slot, float &w, float &bv) {
+                        const int src = (q & 63) + g4;                         // position q + k, k = l >> 4
+                        slot = __shfl(d.x, src);
+                        w = __int_as_float(__shfl(d.y, src));
+                        const uint32_t m = (uint32_t)__shfl(d.z, src);
+                        bv = ((m >> jr) & 1u) ? 1.f : 0.f;
+                    };
+                    // two-deep: group q's rows are in registers and group q + 4's descriptors
+                    // too; each iteration issues the rows of group q + 4 (address known a group
+                    // ahead) and the descriptors of group q + 8 before group q's MFMAs
+                    int slot, slot1;
+                    float w, bv, w1, bv1;
+                    desc(dc, 0, slot, w, bv);
+                    {
+                        const int q1 = 4 < npos ? 4 : 0;
+                        desc(q1 < 64 ? dc : dn, q1, slot1, w1, bv1);
+                    }
+                    const float *xr = lds_tile + slot * (int)CW + 8 * jr;
+                    float4 x0 = *reinterpret_cast<const float4 *>(xr);
+                    float4 x1 = *reinterpret_cast<const float4 *>(xr + 4);
+                    int base = 0;                  // dc holds positions [base, base + 64), dn the next 64
+                    for (int q = 0; q < npos; q += 4) {
+                        if (NIIDMIX_MF_SPLIT == 3) break;                     // tuning builds only
+                        // rows of group q + 4 (a dummy re-read of group q's on the last group)
+                        const float *xrn = lds_tile + slot1 * (int)CW + 8 * jr;
+                        const float4 y0 = *reinterpret_cast<const float4 *>(xrn);
+                        const float4 y1 = *reinterpret_cast<const float4 *>(xrn + 4);
+                        // descriptors of group q + 8
+                        const int q2 = q + 8 < npos ? q + 8 : q;
+                        if (q2 >= base + 64) {                                 // wave-uniform
+                            dc = dn;
+                            base += 64;
+                            if (base + 64 < npos) dn = ldd(base + 64);
                         }
+                        int slot2;
+                        float w2, bv2;
+                        desc(q2 >= base ? dc : dn, q2, slot2, w2, bv2);
+                        const float a[8] = {w * x0.x, w * x0.y, w * x0.z, w * x0.w,
+                                            w * x1.x, w * x1.y, w * x1.z, w * x1.w};
+#pragma unroll
+                        for (int cb = 0; cb < 8; ++cb)
+                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cb], bv, acc[cb], 0, 0, 0);
+                        x0 = y0;
+                        x1 = y1;
+                        w = w1;
+                        bv = bv1;
+                        slot1 = slot2;
+                        w1 = w2;
+                        bv1 = bv2;
                     }
                     // update_models: o = z + acc (z from the row's own staged value), in place
 #pragma unroll

@@ -205,7 +205,7 @@ def test_tile_lds_segment_loop_bitwise(name, gpu, oracle_mod):
         assert ok, (name, worst)
 
 
-@pytest.mark.parametrize("mf_waves", ["", "3"])
+@pytest.mark.parametrize("mf_waves", ["", "3", "-3"])
 @pytest.mark.parametrize("name", golden_cases())
 def test_tile_lds_mfma_bitwise(name, mf_waves, gpu, oracle_mod, monkeypatch):
     """The exact matrix-core path (v_mfma_f32_16x16x4_f32 with 0/1 row masks; blocks whose staged
@@ -215,7 +215,8 @@ def test_tile_lds_mfma_bitwise(name, mf_waves, gpu, oracle_mod, monkeypatch):
     g = load_golden(name)
     if g["x"].shape[1] % 2:
         pytest.skip("odd p: the LDS tile kernel reads column pairs")
-    if mf_waves:      # the first 3 waves of a block on the matrix cores, the rest walk segments
+    if mf_waves:      # "3": the first 3 waves of a block on the matrix cores, the rest walk
+        # segments; "-3": every 3rd column chunk's blocks on the matrix cores, the others walk
         monkeypatch.setenv("NIIDMIX_TLDS_MF_WAVES", mf_waves)
     m = _tile_lds_mixer(g, gpu, 16)
     assert m.tmf is not None and m.tmf.lp is m.tlds
