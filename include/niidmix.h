@@ -280,6 +280,13 @@ typedef struct niidmix_tile_lds_plan {
      *   entry: slot, weight (fp32 bits), tile rows that take it, 0 */
     const int32_t *mf_ptr;
     const int32_t *mf;
+    /* optional (rt 16 with segments, mf_ptr NULL; NULL = every source staged in LDS): REGISTER
+     * rows, sources outside a group that only masked entries read (a gateway row's inter-clique
+     * neighbour), kept per tile in registers instead of the LDS stage
+     * (niidmix.tile.build_tile_lds_plan(remote_regs=True)):  rem_rows [n_sub * 16] int32 global
+     * rows of each tile's register rows (-1 unused); a masked segment whose word 0 has bit 29 set
+     * reads register row (word 0 & 0xfff).  Round 4 (ABI 4). */
+    const int32_t *rem_rows;
 } niidmix_tile_lds_plan;
 
 int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

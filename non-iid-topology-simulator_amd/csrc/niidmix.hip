@@ -1823,7 +1823,23 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     "v_fma_f32 v33, %[q1], s43, v33\n\t"                                                             \
     "s_set_gpr_idx_off\n\t"                                                                          \
     "s_branch .Lmsk_loop_%=\n\t"
-#define NIIDMIX_SEG_WALK(UPD, MSK)                                                                   \
+// REGISTER rows (plans with rem_rows): a masked entry whose word 0 has bit 29 set takes its source
+// from the tile's register rows, pinned in v[64:95] (register row i in v[64 + 2i : 65 + 2i]),
+// picked by GPR-index mode, instead of from the LDS stage.
+#define NIIDMIX_SEG_REMOTE                                                                           \
+    "s_bitcmp1_b32 s41, 29\n\t"                                                                     \
+    "s_cbranch_scc0 .Lw_lds_%=\n\t"                                                                 \
+    "s_and_b32 s46, s41, 0xfff\n\t"                                                                 \
+    "s_lshl_b32 s46, s46, 1\n\t"                                                                    \
+    "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
+    "v_mov_b32 %[q0], v64\n\t"                                                                      \
+    "v_mov_b32 %[q1], v65\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                         \
+    "s_branch .Lw_mskgo_%=\n"                                                                       \
+    ".Lw_lds_%=:\n\t"
+#define NIIDMIX_REM_IN , [rem] "{v[64:95]}"(rem)
+#define NIIDMIX_SEG_WALK(UPD, MSK) NIIDMIX_SEG_WALK_X(UPD, MSK, "", )
+#define NIIDMIX_SEG_WALK_X(UPD, MSK, RMSK, RIN)                                                      \
     asm volatile("s_mov_b32 s36, %[sb0]\n"                                                           \
                  ".Lc_next_%=:\n\t"                                                                  \
                  "s_cmp_ge_u32 s36, %[sb1]\n\t"                                                      \
@@ -1870,9 +1886,11 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  NIIDMIX_SEG_SKIPBLK("%[x2]", "2", UPD)                                               \
                  NIIDMIX_SEG_SKIPBLK("%[x3]", "3", UPD)                                               \
                  "\n.Lw_masked_%=:\n\t"                                                              \
+                 RMSK                                                                                \
                  "ds_read_b32 %[q0], %[va]\n\t"                                                      \
                  "ds_read_b32 %[q1], %[va] offset:4\n\t"                                             \
-                 "s_waitcnt lgkmcnt(0)\n\t"                                                          \
+                 "s_waitcnt lgkmcnt(0)\n"                                                             \
+                 ".Lw_mskgo_%=:\n\t"                                                                 \
                  MSK                                                                                 \
                  "\n.Lc_done_%=:\n\t"                                                                \
                  "s_add_u32 s36, s36, 64\n\t"                                                        \
@@ -1885,7 +1903,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                    [dz] "=&v"(dz), [vo] "=&v"(vo)                                                   \
                  : [sp] "s"(segp), [sb0] "s"(sb0), [sb1] "s"(sb1), [ln] "v"(lane), [base] "s"(base), \
                    [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),                          \
-                   [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB)             \
+                   [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB) RIN         \
                  : "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", \
                    "s47", "m0", "scc", "memory")
 // segp: the segment words (int4 per segment); the tile's segments [sb0, sb1) are fetched 64 at a time
@@ -1899,6 +1917,21 @@ __device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int
     uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
     if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
     else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
+    (void)pr;
+}
+typedef float Rem32 __attribute__((ext_vector_type(32)));
+// the same walker with the tile's register rows (rem) pinned in v[64:95]
+template <bool EXACT, int RB>
+__device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp, int sb0, int sb1,
+                                                int base, int w0, int w1, int lane8, int lane,
+                                                const Rem32 &rem) {
+    static_assert(5 * RB < 65536, "ds_read immediate offset");
+    uint64_t x0, x1, x2, x3, pr;
+    uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
+    if constexpr (EXACT)
+        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
+    else
+        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
     (void)pr;
 }
 
@@ -2050,7 +2083,7 @@ inline size_t tlds_slack(bool seg, int cw) {
 }
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
-template <bool EXACT, int RT, int SV, int RS, bool SEG>
+template <bool EXACT, int RT, int SV, int RS, bool SEG, bool REM = false>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
@@ -2060,7 +2093,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
     const int32_t *__restrict__ seg_ptr, const int32_t *__restrict__ seg,
     const float *__restrict__ seg_w, const int32_t *__restrict__ mf_ptr,
-    const int32_t *__restrict__ mf, int mf_waves) {
+    const int32_t *__restrict__ mf, int mf_waves, const int32_t *__restrict__ rem_rows) {
     // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
     // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
@@ -2150,8 +2183,24 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 }
         }
     }
+    // register rows of this wave's tile (plans with rem_rows): loaded while the stage lands, so
+    // the barrier's wait covers them; lanes past the item re-read a valid column
+    Rem32 rem;
+    if constexpr (REM) {
+        const int sub = grp_tile_ptr[grp] + wave;
+        const int subc = sub < grp_tile_ptr[grp + 1] ? sub : grp_tile_ptr[grp];
+        const int sl_ = lane < rs ? lane : rs - 1;
+        const int64_t cr = c0 + 2 * sl_ < p ? c0 + 2 * sl_ : c0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = rem_rows[subc * 16 + r];
+            const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cr);
+            rem[2 * r] = v.x;
+            rem[2 * r + 1] = v.y;
+        }
+    }
     __syncthreads();
-    if constexpr (NIIDMIX_TLDS_MF && EXACT && SEG && RT == 16 && NIIDMIX_TLDS_SPLIT == 0) {
+    if constexpr (NIIDMIX_TLDS_MF && EXACT && SEG && RT == 16 && NIIDMIX_TLDS_SPLIT == 0 && !REM) {
         // 2'. Matrix-core path (exact): v_mfma_f32_16x16x4_f32 applies 4 positions to the tile's 16
         // rows x 16 columns at a time as a k-ordered chain of single-rounding fmas: A[col][k] =
         // fl(w_k * x_k[col]), B[k][row] = 1 if the row takes position k else 0, so a row that
@@ -2382,7 +2431,11 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 // it, its weight (fp32 bits).  One walker for every tile: walkers specialised by the
                 // tile's row count (4 / 8 / 12 / 16 pairs) measured no faster, and their four call
                 // sites made hipcc keep a second copy of the tuple (90 VGPRs, two blocks per CU)
-                tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0, w1,
+                if constexpr (REM)
+                    tlds16_walk_rem<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0,
+                                                                 w1, lane8, lane, rem);
+                else
+                    tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0, w1,
                                                              lane8, lane);
                 goto tile_epilogue;
             }
@@ -3460,6 +3513,10 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     if (seg && (!plan->seg || !plan->seg_w)) return set_error(NIIDMIX_EINVAL, "null segment arrays");
     // matrix-core path (exact mode, segment plans only: the walker is its per-block fallback)
     const bool mf = seg && mode == NIIDMIX_MODE_EXACT && plan->mf_ptr != nullptr;
+    // register rows (rem_rows): the segment walker only (the other loops read every source from LDS)
+    const bool rem = plan->rem_rows != nullptr;
+    if (rem && (!seg || plan->mf_ptr != nullptr))
+        return set_error(NIIDMIX_EINVAL, "rem_rows needs the segment walker (seg_ptr set, mf_ptr NULL)");
     if (mf && !plan->mf) return set_error(NIIDMIX_EINVAL, "null MFMA position list");
     // waves of a block on the matrix cores (the rest walk segments on the VALU side by side);
     // NIIDMIX_TLDS_MF_WAVES overrides (tuning), default every wave
@@ -3486,11 +3543,12 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const size_t lds = (size_t)stage_rows * cw * sizeof(float) + tlds_slack(seg, cw);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = seg ? (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16)>) \
+        auto kfn = seg ? (rem ? (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16), (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16), (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16), (R == 16)>) \
+                              : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16)>)) \
                        : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, false> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, false> : k_mix_tile_lds<E, R, V, 64, false>); \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf, mf_waves); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf, mf_waves, plan->rem_rows); \
     } while (0)
 #define NIIDMIX_TLDS_V(E, R) do { if (sv == 4) NIIDMIX_TLDS(E, R, 4); else NIIDMIX_TLDS(E, R, 2); } while (0)
 #define NIIDMIX_TLDS_R(E) do { if (plan->rt == 8) NIIDMIX_TLDS_V(E, 8); else if (plan->rt == 16) NIIDMIX_TLDS_V(E, 16); else NIIDMIX_TLDS_V(E, 32); } while (0)

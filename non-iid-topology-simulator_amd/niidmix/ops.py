@@ -322,11 +322,13 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                  grp_src_ptr: torch.Tensor, grp_src_rows: torch.Tensor, out: torch.Tensor, rt: int,
                  max_src: int, max_tiles: int, mode: int, seg_ptr: Optional[torch.Tensor] = None,
                  seg: Optional[torch.Tensor] = None, seg_w: Optional[torch.Tensor] = None,
-                 mf_ptr: Optional[torch.Tensor] = None, mf: Optional[torch.Tensor] = None) -> None:
+                 mf_ptr: Optional[torch.Tensor] = None, mf: Optional[torch.Tensor] = None,
+                 rem_rows: Optional[torch.Tensor] = None) -> None:
     """seg_ptr / seg / seg_w: the plan's segments (niidmix.tile.build_tile_segments, RT 16 only):
     the kernel's segment loop instead of the per-position loop; bit-identical results.
     mf_ptr / mf: its MFMA position lists (niidmix.tile.build_tile_mfma_positions; needs the
-    segments, exact mode): the matrix-core path, bit-identical, the walker its per-block fallback."""
+    segments, exact mode): the matrix-core path, bit-identical, the walker its per-block fallback.
+    rem_rows: the plan's register rows (build_tile_lds_plan(remote_regs=True); segments only)."""
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -358,13 +360,19 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
         _vec("mf", mf, torch.int32, dev)
         _req(mf.numel() % 4 == 0 and mf.data_ptr() % 16 == 0, "mf: [E, 4] int32, 16-B aligned")
         mfs = (mf_ptr.data_ptr(), mf.data_ptr() if mf.numel() else mf_ptr.data_ptr())
+    rem = None
+    if rem_rows is not None:
+        _req(seg_ptr is not None and mf_ptr is None,
+             "register rows: with the segments and without the MFMA position lists")
+        _vec("rem_rows", rem_rows, torch.int32, dev, t * 16)       # rows < x.shape[0]: the plan's
+        rem = rem_rows.data_ptr()
     _no_overlap(x, out)
     some = sub_ptr.data_ptr()
     plan = _lib.TileLdsPlanC(t, int(rt), g, int(max_src), int(max_tiles), sub_ptr.data_ptr(),
                              sub_rows.data_ptr(), sub_slot.data_ptr(), sub_wself.data_ptr(),
                              pos_slot.data_ptr() or some, pos_mask.data_ptr() or some,
                              pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
-                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs, *mfs)
+                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs, *mfs, rem)
     rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
                                            out.shape[0], x.shape[1], ctypes.byref(plan), int(mode),
                                            _stream(x))
@@ -481,7 +489,7 @@ _LAZY = {
     "l_sub_slot": "tlds", "l_sub_wself": "tlds", "l_pos_slot": "tlds", "l_pos_mask": "tlds",
     "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
     "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
-    "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds",
+    "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds", "l_rem_rows": "tlds",
     "w_dense": "dense",
     "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell", "band": "ell",
 }
@@ -619,6 +627,17 @@ class Mixer:
                 grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
             self.tlds, self.tlds_reason = self._hosted(
                 ("tlds", rt), lambda: build_tile_lds_plan(csr, grp, rt))
+            # register rows for sources outside a group that only masked entries read, when the
+            # stage would otherwise not fit three 120-column blocks per CU (10 000 d-cliques nodes:
+            # 199 staged rows -> 100, 128-column items); NIIDMIX_TLDS_REMOTE=0 / 1 forces it
+            rem = os.environ.get("NIIDMIX_TLDS_REMOTE", "auto")
+            lp0 = self.tlds
+            if (lp0 is not None and rt == 16 and rem != "0" and
+                    (rem == "1" or (lp0.max_src + 2) * 480 + 64 > (160 * 1024) // 3)):
+                lr, _ = self._hosted(("tlds_rem", rt),
+                                     lambda: build_tile_lds_plan(csr, grp, rt, remote_regs=True))
+                if lr is not None and lr.rem_rows is not None:
+                    self.tlds = lr
         if self.tlds is None:
             return
         lp = self.tlds
@@ -657,6 +676,8 @@ class Mixer:
             self.s_seg_ptr = torch.from_numpy(ts.seg_ptr).to(dev)
             self.s_seg = torch.from_numpy(np.ascontiguousarray(ts.seg).reshape(-1)).to(dev)
             self.s_seg_w = torch.from_numpy(np.ascontiguousarray(ts.seg_w).reshape(-1)).to(dev)
+        self.l_rem_rows = (torch.from_numpy(lp.rem_rows).to(dev) if lp.rem_rows is not None
+                           else None)
         self.tmf = tm if ts is not None else None
         if self.tmf is not None:
             self.m_mf_ptr = torch.from_numpy(tm.mf_ptr).to(dev)
@@ -797,9 +818,16 @@ class Mixer:
             ts = self.tseg
             segs = (self.s_seg_ptr, self.s_seg, self.s_seg_w) if \
                 self.use_segments and ts is not None and ts.lp is lp else ()
-            if segs and k == "tile-lds-exact" and self.use_mfma and self.tmf is not None \
-                    and self.tmf.lp is lp:
+            rem = None
+            if lp.rem_rows is not None:
+                _req(bool(segs), "a plan with register rows needs the segment walker "
+                     "(use_segments; NIIDMIX_TLDS_REMOTE=0 builds a plan without them)")
+                rem = self.l_rem_rows
+            if segs and rem is None and k == "tile-lds-exact" and self.use_mfma and \
+                    self.tmf is not None and self.tmf.lp is lp:
                 segs = segs + (self.m_mf_ptr, self.m_mf)
+            if rem is not None:
+                segs = segs + (None, None, rem)
             mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
                          self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
                          self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,

@@ -243,6 +243,8 @@ def build_tile_plan(csr, groups=None, rt=16, max_rows=None):
 
 LDS_MAX_SRC = 256
 LDS_MAX_WAVES = {8: 16, 16: 8, 32: 4}
+POS_REMOTE = 1 << 29           # pos_slot flag: the source is one of the tile's register rows
+REM_MAX = 16                   # register rows per tile (rem_rows[t * REM_MAX + i])
 
 
 @dataclass
@@ -257,15 +259,56 @@ class TileLdsPlan:
     grp_src_rows: np.ndarray  # int32 [sum of group source counts]
     max_src: int
     max_tiles: int
+    rem_rows: np.ndarray = None   # int32 [T * REM_MAX] register rows per tile (-1: none), or None
 
     @property
     def n_grp(self):
         return len(self.grp_tile_ptr) - 1
 
 
-def build_tile_lds_plan(csr, groups=None, rt=8):
+def _register_sources(tp, t0, t1, srcs, members, row_mask):
+    """{tile: [source rows]} of a group's sources kept in REGISTERS instead of the LDS stage: a
+    source outside the group (a gateway row's inter-clique neighbour) whose every position is
+    taken by at most all-but-two rows of its tile -- so the segment builder can never make it part
+    of a run (runs read consecutive LDS slots) -- at most REM_MAX per tile, in list order.  At
+    10 000 d-cliques nodes each clique reads 99 such rows, one per gateway member: staging them
+    doubled the stage (199 rows), left room for 96-column items only, and each is read once."""
+    rt = tp.rt
+    ok = {int(v) for v in srcs if int(v) not in members}
+    per_tile = {}
+    for t in range(t0, t1):
+        real = 0
+        for r in range(rt):
+            if tp.sub_rows[t * rt + r] >= 0:
+                real |= 1 << r
+        n_real = bin(real).count("1")
+        for k in range(int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])):
+            v = int(tp.pos_src[k]) & row_mask
+            if v in ok and bin(int(tp.pos_mask[k]) & real).count("1") > n_real - 2:
+                ok.discard(v)
+    for t in range(t0, t1):
+        lst = []
+        for k in range(int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])):
+            v = int(tp.pos_src[k]) & row_mask
+            if v in ok and v not in lst:
+                lst.append(v)
+        per_tile[t] = lst
+    # a source two tiles read, or a tile with too many, stays staged
+    seen = {}
+    for t, lst in per_tile.items():
+        for v in lst:
+            seen[v] = seen.get(v, 0) + 1
+    for t in per_tile:
+        lst = [v for v in per_tile[t] if seen[v] == 1]
+        per_tile[t] = lst[:REM_MAX]
+    return per_tile
+
+
+def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False):
     """(plan, None) or (None, reason): build_tile_plan over `groups`, then per group the sorted list
-    of distinct source rows (every row its tiles read, self rows included) and the slot indices."""
+    of distinct source rows (every row its tiles read, self rows included) and the slot indices.
+    remote_regs (RT 16, segment walker only): sources outside a group that only MASKED entries
+    read (_register_sources) are loaded into registers per tile (rem_rows) instead of staged."""
     if rt not in LDS_MAX_WAVES:
         return None, f"rt={rt} not in {tuple(LDS_MAX_WAVES)}"
     if groups:
@@ -298,6 +341,8 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
     sub_slot = np.zeros_like(tp.sub_rows)
     src_ptr, src_rows = [0], []
     max_src = max_tiles = 0
+    remote = remote_regs and rt == 16
+    rem_rows = np.full(tp.n_sub * REM_MAX, -1, np.int32) if remote else None
     for gi in range(len(gtp) - 1):
         t0, t1 = int(gtp[gi]), int(gtp[gi + 1])
         p0, p1 = int(tp.sub_ptr[t0]), int(tp.sub_ptr[t1])
@@ -307,14 +352,28 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
         seq = np.concatenate([tp.pos_src[p0:p1] & row_mask, rows[rows >= 0]])
         _, first = np.unique(seq, return_index=True)
         srcs = seq[np.sort(first)]
+        reg_of = {}                                   # (tile, source) -> register index
+        if remote:
+            per_tile = _register_sources(tp, t0, t1, srcs, {int(r) for r in rows[rows >= 0]},
+                                         row_mask)
+            in_regs = set()
+            for t, lst in per_tile.items():
+                for i, v in enumerate(lst):
+                    reg_of[(t, v)] = i
+                    rem_rows[t * REM_MAX + i] = v
+                    in_regs.add(v)
+            srcs = np.asarray([v for v in srcs if int(v) not in in_regs], srcs.dtype)
         if len(srcs) > LDS_MAX_SRC:
             return None, f"group {gi} reads {len(srcs)} distinct rows (> {LDS_MAX_SRC})"
         if t1 - t0 > LDS_MAX_WAVES[rt]:
             return None, f"group {gi} has {t1 - t0} tiles of {rt} rows (> {LDS_MAX_WAVES[rt]})"
         slot_of = {int(r): i for i, r in enumerate(srcs)}
-        for k in range(p0, p1):
-            v = int(tp.pos_src[k])
-            pos_slot[k] = slot_of[v & row_mask] | (v & POS_UNIFORM)
+        for t in range(t0, t1):
+            for k in range(int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])):
+                v = int(tp.pos_src[k])
+                ri = reg_of.get((t, v & row_mask))
+                pos_slot[k] = (POS_REMOTE | ri if ri is not None else slot_of[v & row_mask]) | \
+                    (v & POS_UNIFORM)
         for k in range(t0 * rt, t1 * rt):
             r = int(tp.sub_rows[k])
             sub_slot[k] = slot_of[r] if r >= 0 else 0
@@ -322,11 +381,14 @@ def build_tile_lds_plan(csr, groups=None, rt=8):
         src_ptr.append(len(src_rows))
         max_src = max(max_src, len(srcs))
         max_tiles = max(max_tiles, t1 - t0)
+    if remote and not np.any(rem_rows >= 0):
+        rem_rows = None                               # nothing to keep in registers
     return TileLdsPlan(tile=tp, pos_slot=pos_slot, sub_slot=sub_slot,
                        grp_tile_ptr=np.asarray(gtp, np.int32),
                        grp_src_ptr=np.asarray(src_ptr, np.int32),
                        grp_src_rows=np.asarray(src_rows, np.int32),
-                       max_src=max(max_src, 1), max_tiles=max(max_tiles, 1)), None
+                       max_src=max(max_src, 1), max_tiles=max(max_tiles, 1),
+                       rem_rows=rem_rows), None
 
 
 def apply_np(plan, x, exact=True, average_only=False):
@@ -347,6 +409,7 @@ def apply_np(plan, x, exact=True, average_only=False):
 
 
 SEG_HARD = 1 << 30           # seg word 0 flag: a MASKED position (rows in word 1, weight in word 2)
+SEG_REMOTE = 1 << 29         # with SEG_HARD: the source is register row (word 0 & SEG_SLOT)
 SEG_WORDS = 4
 SEG_SLOT = 0xfff             # slot field of word 0
 
@@ -385,7 +448,8 @@ def build_tile_segments(lp, max_len=32):
     full = (1 << rt) - 1
     if lp.max_src + 2 > SEG_SLOT:
         return None
-    slots = (lp.pos_slot & (POS_UNIFORM - 1)).astype(np.int64)
+    slots = (lp.pos_slot & (POS_REMOTE - 1)).astype(np.int64)
+    remote = (lp.pos_slot & POS_REMOTE) != 0
     uni = (lp.pos_slot & POS_UNIFORM) != 0
     mask = tp.pos_mask.astype(np.int64)
     w0s = tp.pos_w.reshape(-1, rt)[:, 0] if tp.n_pos else np.zeros(0, np.float32)
@@ -410,6 +474,8 @@ def build_tile_segments(lp, max_len=32):
             miss = int(~mask[k] & full)
             wk = np.float32(w0s[k]).view(np.uint32)
             easy = bool(uni[k]) and (miss & (miss - 1)) == 0 and wk in wbits
+            if remote[k]:
+                assert not easy, "a register row must be a masked entry (_register_sources)"
             if not easy:
                 if cur is not None:
                     segs.append(cur)
@@ -424,7 +490,7 @@ def build_tile_segments(lp, max_len=32):
                         classes.setdefault(int(np.float32(wr[r]).view(np.uint32)), 0)
                         classes[int(np.float32(wr[r]).view(np.uint32))] |= 1 << r
                 for wb, cm in classes.items():
-                    segs.append(["M", int(slots[k]), cm, wb])
+                    segs.append(["M", int(slots[k]) | (SEG_REMOTE if remote[k] else 0), cm, wb])
                 continue
             skip = miss.bit_length() - 1 if miss else -1
             sel = 1 if (wk == wbits[1] and wk != wbits[0]) else 0
@@ -486,7 +552,10 @@ def segments_row_lists(lp, ts):
         for s in seg[ts.seg_ptr[t]:ts.seg_ptr[t + 1]]:
             hd = int(s[0])
             if hd & SEG_HARD:
-                src = int(src_rows[base + (hd & SEG_SLOT)])
+                if hd & SEG_REMOTE:
+                    src = int(lp.rem_rows[t * REM_MAX + (hd & SEG_SLOT)])
+                else:
+                    src = int(src_rows[base + (hd & SEG_SLOT)])
                 m, w = int(s[1]), np.uint32(s[2]).view(np.float32)
                 for r in lists:
                     if (m >> r) & 1:
@@ -538,7 +607,7 @@ def build_tile_mfma_positions(lp):
     """TileMfmaPositions of a TileLdsPlan (RT 16 tiles)."""
     tp = lp.tile
     rt = tp.rt
-    if rt != 16:
+    if rt != 16 or lp.rem_rows is not None:      # the matrix-core path reads every source from LDS
         return None
     slots = (lp.pos_slot & (POS_UNIFORM - 1)).astype(np.int64)
     uni = (lp.pos_slot & POS_UNIFORM) != 0

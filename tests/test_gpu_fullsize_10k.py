@@ -7,9 +7,10 @@ layouts and launch paths as bench.py --config dcliques10000 and the multi-GPU st
     against the oracle (the last starts 1.05e10 elements into the slab: past 2^31, 2^32 and 2^33),
     plus column-sum preservation over every block; and the same on the round-2 layout
     [4096, 10000, 256] (NIIDMIX_Q_BLOCK_COLS=256);
-  * the exact default (tile-lds-exact, 199 staged rows per clique -> 96-column items) on row-major
-    [10000, 2^20] slabs, bitwise on windows that straddle item boundaries, the ragged last item and
-    rows whose offsets exceed 2^33 elements;
+  * the exact default (tile-lds-exact: since round 4 each clique's 99 inter-clique sources are
+    register rows, 100 staged rows -> 128-column items; NIIDMIX_TLDS_REMOTE=0 stages all 199 rows ->
+    96-column items) on row-major [10000, 2^20] slabs, bitwise on windows that straddle item
+    boundaries, the ragged last item and rows whose offsets exceed 2^33 elements;
   * one rank of the 8000-node weak N=8 column-stripe shape (StripedMixer: 79 gateway terms per
     clique, B = 64), windows against the oracle and column sums over the whole stripe.
 
@@ -82,22 +83,27 @@ def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod, monkeypatch
     _free()
 
 
-def test_dcliques10000_tile_lds_exact_rowmajor(dc10k, gpu, oracle_mod):
+@pytest.mark.parametrize("remote", ["auto", "0"])
+def test_dcliques10000_tile_lds_exact_rowmajor(remote, dc10k, gpu, oracle_mod, monkeypatch):
     from niidmix import memory, ops
+    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", remote)
     csr, cliques = dc10k
     m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
     assert m.kernel_for("exact") == "tile-lds-exact"
-    assert m.tlds.max_src == 199
+    if remote == "auto":
+        assert m.tlds.max_src == 100 and m.tlds.rem_rows is not None
+        cw = 128           # 102 x 128 x 4 B = 52 KB per block; P = 2^20 = 8192 x 128: exact items
+    else:
+        assert m.tlds.max_src == 199 and m.tlds.rem_rows is None
+        cw = 96            # 199 x 96 x 4 B = 76 KB: two blocks per CU; 2^20 = 10922 x 96 + 64
     x = memory.empty_slab(10000, P_FULL, gpu)
     x.normal_(generator=torch.Generator(device=gpu).manual_seed(11))
     y = memory.empty_slab(10000, P_FULL, gpu)
     y.fill_(float("nan"))
     m(x, out=y, mode="exact")
     torch.cuda.synchronize()
-    # 96-column items (199 rows x 96 cols x 4 B = 76 KB: two blocks per CU); P = 2^20 = 10922 x 96
-    # + 64, so the last item is ragged
-    w = 96 * 3
-    for c0 in (0, 96 * 5461 - 40, P_FULL - w):
+    w = cw * 3
+    for c0 in (0, cw * 5461 - 40, P_FULL - w):
         xw = x[:, c0:c0 + w].cpu().numpy()
         ref = oracle_mod.mix_exact_c(xw, csr.row_ptr, csr.col, csr.val)
         assert oracle_mod.bitwise_equal(y[:, c0:c0 + w].cpu().numpy(), ref), c0

@@ -660,3 +660,33 @@ def test_blocked_overlap_checks_use_each_block_stride(gpu):
     out_ok = torch.as_strided(flat, (2, rows, bc), (r_, bc, 1))[:, :, :]
     out_ok = torch.zeros(3 * r_, device=gpu).as_strided((2, rows, bc), (int(1.5 * r_), bc, 1))
     m.mix_blocked(x, out_ok, 2 * bc)
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("name", golden_cases("dcliques"))
+def test_tile_lds_register_rows_vs_golden(name, mode, gpu, oracle_mod, monkeypatch):
+    """Plans whose out-of-group sources only masked entries read keep them in registers
+    (NIIDMIX_TLDS_REMOTE=1: build_tile_lds_plan(remote_regs=True), the 10 000-node default):
+    bitwise the reference in exact mode (non-finite fixtures included: inf / NaN in a gateway's
+    neighbour reach the output only through the register row), within the tolerance in fast
+    mode; the stage holds fewer rows than the all-staged plan."""
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", "0")
+    m0 = _mixer(g, gpu)
+    if m0.tlds is None:
+        pytest.skip(m0.tlds_reason)
+    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", "1")
+    m = _mixer(g, gpu)
+    if m.tlds.rem_rows is None:
+        pytest.skip("no source qualifies for a register row")
+    assert m.tlds.max_src < m0.tlds.max_src and m.tmf is None
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-lds-" + mode).cpu().numpy()
+    if mode == "exact":
+        assert oracle_mod.bitwise_equal(y, g["y"]), name
+    else:
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+        assert ok, (name, worst)
