@@ -186,15 +186,32 @@ class ShardPlan:
         return [self._halo_of(r)[0] for r in range(self.world)]
 
 
+class _StagedHandle:
+    """A gloo exchange of HIP tensors staged through host buffers (rehearsal only): the works, and
+    the (host buffer, device rows) pairs to copy back once they completed."""
+
+    def __init__(self, works, back):
+        self.works, self.back = works, back
+
+
 class DistTransport:
     """Halo exchange over torch.distributed point-to-point (RCCL on GPUs, gloo on CPU): per window,
     one grouped batch_isend_irecv with every peer.  A peer's exclusive rows go straight out of the
-    slab (one contiguous block, no copy); rows several peers read are packed (index_select)."""
+    slab (one contiguous block, no copy); rows several peers read are packed (index_select).
+
+    With the gloo backend and HIP tensors (NIIDMIX_BENCH_BACKEND=gloo: several ranks rehearsing on
+    one GPU, where RCCL refuses two ranks per device) every message is staged through host memory;
+    the RCCL path never is."""
 
     def __init__(self, group=None):
         self.group = group
 
+    def _staged(self, xk):
+        return xk.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def exchange(self, sm, k, xk):
+        if self._staged(xk):
+            return self._exchange_staged(sm, k, xk)
         ops = []
         sh = sm.shard
         for q in sorted(set(sh.send_block) | set(sh.send_shared) | set(sh.recv)):
@@ -213,8 +230,33 @@ class DistTransport:
                     ops.append(dist.P2POp(dist.irecv, xk[r0 + nb:r0 + nb + ns], q, group=self.group))
         return dist.batch_isend_irecv(ops) if ops else []
 
+    def _exchange_staged(self, sm, k, xk):
+        ops, back = [], []
+        sh = sm.shard
+        for q in sorted(set(sh.send_block) | set(sh.send_shared) | set(sh.recv)):
+            a, b = sh.send_block.get(q, (0, 0))
+            if b > a:
+                ops.append(dist.P2POp(dist.isend, xk[a:b].cpu(), q, group=self.group))
+            if q in sm.shared_idx:
+                ops.append(dist.P2POp(dist.isend, torch.index_select(
+                    xk[:sm.n_local], 0, sm.shared_idx[q]).cpu(), q, group=self.group))
+            if q in sh.recv:
+                r0, nb, ns = sh.recv[q]
+                for a0, n0 in ((r0, nb), (r0 + nb, ns)):
+                    if n0:
+                        buf = torch.empty((n0, xk.shape[1]), dtype=xk.dtype)
+                        ops.append(dist.P2POp(dist.irecv, buf, q, group=self.group))
+                        back.append((buf, xk[a0:a0 + n0]))
+        return _StagedHandle(dist.batch_isend_irecv(ops) if ops else [], back)
+
     @staticmethod
     def wait(handle):
+        if isinstance(handle, _StagedHandle):
+            for wk in handle.works:
+                wk.wait()
+            for buf, dst in handle.back:
+                dst.copy_(buf)
+            return
         for wk in handle:
             wk.wait()                          # NCCL: the current stream waits, not the host
 
