@@ -2616,20 +2616,25 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         }
         }
     tile_epilogue:
-        // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc)
+        // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc).  Four rows at a time: their
+        // own staged values are read together (an unused slot reads slot 0), then combined and
+        // stored, so the LDS latency is paid once per four rows instead of once per row
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-            const int row = __builtin_amdgcn_readlane(d_row, r);
-            if (row < 0) continue;                                  // wave-uniform
-            f2 o = acc.get(r);
-            if (!avg_only) {
-                const f2 xs = stage[__builtin_amdgcn_readlane(d_slot, r) * rs + sl];
-                o = xs * 0.f + o;
-            }
-            if (ok) {
-                float *dst = y + (int64_t)row * ld_y + col;
-                __builtin_nontemporal_store(o.x, dst);
-                __builtin_nontemporal_store(o.y, dst + 1);
+        for (int r0 = 0; r0 < RT; r0 += 4) {
+            f2 xs[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xs[u] = stage[__builtin_amdgcn_readlane(d_slot, r0 + u) * rs + sl];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int row = __builtin_amdgcn_readlane(d_row, r0 + u);
+                if (row < 0) continue;                              // wave-uniform
+                f2 o = acc.get(r0 + u);
+                if (!avg_only) o = xs[u] * 0.f + o;
+                if (ok) {
+                    float *dst = y + (int64_t)row * ld_y + col;
+                    __builtin_nontemporal_store(o.x, dst);
+                    __builtin_nontemporal_store(o.y, dst + 1);
+                }
             }
         }
     }
