@@ -75,6 +75,8 @@ def parse():
                     choices=["fully-connected", "smallworld", "ring"],
                     help="multi-GPU global d-cliques interclique topology")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold-cache", action="store_true",
+                    help="skip the cold-cache single-round timing of graph-replayed configs")
     ap.add_argument("--cpu-sample-nodes", type=int, default=0,
                     help="bound the CPU baseline to the first K nodes' averages (0 = full round)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -187,6 +189,34 @@ def stream_copy_probe(numel, dev, iters=10):
     torch.cuda.synchronize()
     del a, b
     return 2 * numel * 4 * iters / (s.elapsed_time(e) / 1e3) / 1e9
+
+
+def cold_cache_rounds(step, xa, xb, dev, rounds=10, flush_bytes=1 << 30):
+    """a cache-resident config (the ring's 24.8 MB slab lives in the 256 MB MALL
+    between graph-replayed rounds) is also timed once cold.  Before each round a 1 GiB scratch
+    buffer is read and written (evicting the MALL and every XCD's L2), then ONE round is timed
+    alone with HIP events on the launch stream; the same single-round timing without the flush is
+    reported beside it (eager launches, so both include one launch's overhead, unlike the graph)."""
+    scratch = torch.zeros(flush_bytes // 4, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for name, flush in (("warm_eager_us", False), ("cold_us", True)):
+        ts = []
+        for _ in range(rounds):
+            if flush:
+                scratch.add_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            step(xa, xb)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ts.append(e0.elapsed_time(e1) * 1e3)
+            xa, xb = xb, xa
+        res[name] = round(float(np.median(ts)), 2)
+    del scratch
+    torch.cuda.empty_cache()
+    res["flush"] = f"{flush_bytes >> 20} MiB read+written before each cold round; median of {rounds}"
+    return res
 
 
 def e2e_rounds(mixer, n, p, dev, rounds=3):
@@ -579,12 +609,17 @@ def run_node_legs(make, intercliques, args, world, rank, dev, dist, backend, sin
             report.append(pending)
             if on_timeout is not None:
                 on_timeout()
+        if rank == 0:
+            print(f"[bench] node-shard leg {ic}: start", file=sys.stderr, flush=True)
         with LegWatchdog(args.leg_timeout, fire, exit_fn):
             info, err = guarded_leg(
                 lambda: node_shard_leg(make, ic, args.steps, args.warmup, dev, dist, backend,
                                        args.seed, single_ms, fixed)[0],
                 dist, world, rank, flag_dev)
         report.append(info if err is None else {"interclique": ic, "error": err})
+        if rank == 0:
+            print(f"[bench] node-shard leg {ic}: {'ok' if err is None else err}",
+                  file=sys.stderr, flush=True)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
     return report
@@ -893,6 +928,8 @@ def main():
             single = single_gpu_round_ms(n1, p, args.interclique, dev, args.steps, args.warmup)
         dist.barrier()
     copy_gbs = stream_copy_probe(n_local * cols_local, dev)
+    cold = (cold_cache_rounds(step, xa, xb, dev)
+            if world == 1 and graph is not None and not args.no_cold_cache else None)
 
     out = None
     if rank == 0:
@@ -956,6 +993,10 @@ def main():
         }
         if e2e is not None:
             out["e2e"] = e2e
+        if cold is not None:
+            # the slab pair fits the MALL, so the graph-replayed rounds run cache-resident
+            out["config"]["cache_resident"] = 2 * n_local * cols_local * 4 < (256 << 20)
+            out["config"]["cold_cache_round"] = cold
         if world > 1 and args.shard == "nodes":
             out["config"]["halo_GB_recv_rank0"] = round(mixer.halo_bytes / 1e9, 3)
             out["config"]["halo_GB_send_rank0"] = round(mixer.send_bytes / 1e9, 3)
