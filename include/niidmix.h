@@ -287,6 +287,9 @@ typedef struct niidmix_tile_lds_plan {
      * rows of each tile's register rows (-1 unused); a masked segment whose word 0 has bit 29 set
      * reads register row (word 0 & 0xfff).  Round 4 (ABI 4). */
     const int32_t *rem_rows;
+    /* register rows the kernel loads per tile: 8 (every tile's rem_rows entries 8..15 are -1; 16
+     * fewer VGPRs, so three 7-wave blocks fit a CU) or 16; 0 = 16 */
+    int32_t rem_regs;
 } niidmix_tile_lds_plan;
 
 int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

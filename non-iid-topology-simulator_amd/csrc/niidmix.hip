@@ -1773,6 +1773,31 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
 // saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
 #define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
+// the same for tiles whose rows all sit in the first 12 / 8 / 4 slots (a 1000-node d-clique's 9
+// gateway rows form their own tile: 12 adds per position instead of 16)
+#define NIIDMIX_ADD4(T)                                                                             \
+    "v_pk_add_f32 v[32:33], v[32:33], " T "\n\tv_pk_add_f32 v[34:35], v[34:35], " T "\n\t"          \
+    "v_pk_add_f32 v[36:37], v[36:37], " T "\n\tv_pk_add_f32 v[38:39], v[38:39], " T "\n\t"
+#define NIIDMIX_ADD8(T)                                                                             \
+    NIIDMIX_ADD4(T)                                                                                 \
+    "v_pk_add_f32 v[40:41], v[40:41], " T "\n\tv_pk_add_f32 v[42:43], v[42:43], " T "\n\t"          \
+    "v_pk_add_f32 v[44:45], v[44:45], " T "\n\tv_pk_add_f32 v[46:47], v[46:47], " T "\n\t"
+#define NIIDMIX_ADD12(T)                                                                            \
+    NIIDMIX_ADD8(T)                                                                                 \
+    "v_pk_add_f32 v[48:49], v[48:49], " T "\n\tv_pk_add_f32 v[50:51], v[50:51], " T "\n\t"          \
+    "v_pk_add_f32 v[52:53], v[52:53], " T "\n\tv_pk_add_f32 v[54:55], v[54:55], " T "\n\t"
+#define NIIDMIX_SEG_UPD_EXACT12(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD12("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT8(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD8("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT4(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD4("%[pr]")
+#define NIIDMIX_UPD_FAST4(XD)                                                                       \
+    NIIDMIX_FMA1("v[32:33]", XD) NIIDMIX_FMA1("v[34:35]", XD) NIIDMIX_FMA1("v[36:37]", XD)            \
+    NIIDMIX_FMA1("v[38:39]", XD)
+#define NIIDMIX_UPD_FAST8(XD)                                                                       \
+    NIIDMIX_UPD_FAST4(XD) NIIDMIX_FMA1("v[40:41]", XD) NIIDMIX_FMA1("v[42:43]", XD)                 \
+    NIIDMIX_FMA1("v[44:45]", XD) NIIDMIX_FMA1("v[46:47]", XD)
+#define NIIDMIX_UPD_FAST12(XD)                                                                      \
+    NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMA1("v[48:49]", XD) NIIDMIX_FMA1("v[50:51]", XD)                 \
+    NIIDMIX_FMA1("v[52:53]", XD) NIIDMIX_FMA1("v[54:55]", XD)
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
     "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
@@ -1838,7 +1863,22 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     "s_branch .Lw_mskgo_%=\n"                                                                       \
     ".Lw_lds_%=:\n\t"
 #define NIIDMIX_REM_IN , [rem] "{v[64:95]}"(rem)
+#define NIIDMIX_REM_IN8 , [rem] "{v[64:79]}"(rem)
 #define NIIDMIX_SEG_WALK(UPD, MSK) NIIDMIX_SEG_WALK_X(UPD, MSK, "", )
+// a run's positions: %[nr] = 16, 12, 8 or 4 rows updated per position (the tile's rows sit in its
+// first nr slots); the 12-, 8- and 4-row loops are copies of the 16-row one with fewer adds
+#define NIIDMIX_SEG_LOOP(S, UPD)                                                                     \
+    ".Lseg_loop" S "_%=:\n\t"                                                                       \
+    NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", S "0", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", S "1", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x2]", "%[x0]", "o4", S "2", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x3]", "%[x1]", "o5", S "3", UPD)                                              \
+    "v_add_u32 %[va], %[o4], %[va]\n\t"                                                             \
+    "s_branch .Lseg_loop" S "_%=\n\t"                                                               \
+    NIIDMIX_SEG_SKIPBLK("%[x0]", S "0", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x1]", S "1", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x2]", S "2", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x3]", S "3", UPD)
 #define NIIDMIX_SEG_WALK_X(UPD, MSK, RMSK, RIN)                                                      \
     asm volatile("s_mov_b32 s36, %[sb0]\n"                                                           \
                  ".Lc_next_%=:\n\t"                                                                  \
@@ -1873,18 +1913,18 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  "s_bfe_u32 s38, s41, 0x8000c\n\t"                                                   \
                  "s_bfe_u32 s46, s41, 0x80014\n\t"                                                   \
                  "s_lshl_b32 s46, s46, 1\n\t"                                                        \
-                 "s_mov_b32 s47, 0\n"                                                                \
-                 ".Lseg_loop_%=:\n\t"                                                                \
-                 NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", "0", UPD)                                    \
-                 NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", "1", UPD)                                    \
-                 NIIDMIX_SEG_POS("%[x2]", "%[x0]", "o4", "2", UPD)                                    \
-                 NIIDMIX_SEG_POS("%[x3]", "%[x1]", "o5", "3", UPD)                                    \
-                 "v_add_u32 %[va], %[o4], %[va]\n\t"                                                 \
-                 "s_branch .Lseg_loop_%=\n\t"                                                        \
-                 NIIDMIX_SEG_SKIPBLK("%[x0]", "0", UPD)                                               \
-                 NIIDMIX_SEG_SKIPBLK("%[x1]", "1", UPD)                                               \
-                 NIIDMIX_SEG_SKIPBLK("%[x2]", "2", UPD)                                               \
-                 NIIDMIX_SEG_SKIPBLK("%[x3]", "3", UPD)                                               \
+                 "s_mov_b32 s47, 0\n\t"                                                              \
+                 "s_cmp_lt_u32 %[nr], 16\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_small_%=\n\t"                                                 \
+                 NIIDMIX_SEG_LOOP("", UPD)                                                           \
+                 "\n.Lseg_small_%=:\n\t"                                                             \
+                 "s_cmp_le_u32 %[nr], 4\n\t"                                                         \
+                 "s_cbranch_scc1 .Lseg_loopq_%=\n\t"                                                 \
+                 "s_cmp_le_u32 %[nr], 8\n\t"                                                         \
+                 "s_cbranch_scc1 .Lseg_looph_%=\n\t"                                                 \
+                 NIIDMIX_SEG_LOOP("t", UPD##12)                                                      \
+                 NIIDMIX_SEG_LOOP("h", UPD##8)                                                       \
+                 NIIDMIX_SEG_LOOP("q", UPD##4)                                                       \
                  "\n.Lw_masked_%=:\n\t"                                                              \
                  RMSK                                                                                \
                  "ds_read_b32 %[q0], %[va]\n\t"                                                      \
@@ -1902,7 +1942,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                    [q0] "=&v"(q0), [q1] "=&v"(q1), [va] "=&v"(va), [dx] "=&v"(dx), [dy] "=&v"(dy),  \
                    [dz] "=&v"(dz), [vo] "=&v"(vo)                                                   \
                  : [sp] "s"(segp), [sb0] "s"(sb0), [sb1] "s"(sb1), [ln] "v"(lane), [base] "s"(base), \
-                   [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [o1] "i"(RB),                          \
+                   [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [nr] "s"(nr), [o1] "i"(RB),            \
                    [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB) RIN         \
                  : "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", \
                    "s47", "m0", "scc", "memory")
@@ -1911,7 +1951,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // init and its walk -- hipcc otherwise moved the pinned tuple out of v[32:63] to make room for it
 template <bool EXACT, int RB>
 __device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int sb0, int sb1, int base,
-                                            int w0, int w1, int lane8, int lane) {
+                                            int w0, int w1, int lane8, int lane, int nr) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
     uint64_t x0, x1, x2, x3, pr;
     uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
@@ -1920,18 +1960,26 @@ __device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int
     (void)pr;
 }
 typedef float Rem32 __attribute__((ext_vector_type(32)));
-// the same walker with the tile's register rows (rem) pinned in v[64:95]
-template <bool EXACT, int RB>
+typedef float Rem16 __attribute__((ext_vector_type(16)));
+template <int NREM> struct RemRegs { typedef Rem32 V; };        // NREM register rows, pairs
+template <> struct RemRegs<8> { typedef Rem16 V; };
+// the same walker with the tile's NREM register rows (rem) pinned in v[64:64 + 2 NREM)
+template <bool EXACT, int RB, int NREM>
 __device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp, int sb0, int sb1,
                                                 int base, int w0, int w1, int lane8, int lane,
-                                                const Rem32 &rem) {
+                                                int nr, const typename RemRegs<NREM>::V &rem) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
+    static_assert(NREM == 8 || NREM == 16, "8 or 16 register rows");
     uint64_t x0, x1, x2, x3, pr;
     uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
-    if constexpr (EXACT)
+    if constexpr (EXACT && NREM == 16)
         NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
-    else
+    else if constexpr (NREM == 16)
         NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
+    else if constexpr (EXACT)
+        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
+    else
+        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
     (void)pr;
 }
 
@@ -2083,20 +2131,24 @@ inline size_t tlds_slack(bool seg, int cw) {
 }
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
-template <bool EXACT, int RT, int SV, int RS, bool SEG, bool REM = false>
+template <bool EXACT, int RT, int SV, int RS, bool SEG, int NREM = 0, bool MF = false>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
     const int32_t *__restrict__ grp_src_rows, const int64_t *__restrict__ sub_ptr,
     const int32_t *__restrict__ sub_rows, const int32_t *__restrict__ sub_slot,
     const float *__restrict__ sub_wself, const int32_t *__restrict__ pos_slot,
-    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int avg_only,
+    const uint32_t *__restrict__ pos_mask, const float *__restrict__ pos_w, int tl_flags,
     const int32_t *__restrict__ seg_ptr, const int32_t *__restrict__ seg,
     const float *__restrict__ seg_w, const int32_t *__restrict__ mf_ptr,
     const int32_t *__restrict__ mf, int mf_waves, const int32_t *__restrict__ rem_rows) {
     // RS = column pairs per item and staged row: 64 (all lanes), or 60 / 48 so that another block
     // fits a CU's LDS (niidmix_mix_tile_lds_f32); lanes >= RS compute nothing that is stored
     constexpr int rs = RS;
+    // tl_flags: bit 0 average only (no z term), bit 1 every tile walks all 16 rows (tuning A/B of
+    // the walker's 8- / 4-row loops)
+    const bool avg_only = (tl_flags & 1) != 0;
+    const bool small_loops = (tl_flags & 2) == 0;
     constexpr int64_t CW = 2 * RS;               // columns per item
     constexpr uint32_t FULL = (uint32_t)((1ull << RT) - 1ull);
     constexpr int D = 4;                         // positions read together
@@ -2185,14 +2237,15 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     }
     // register rows of this wave's tile (plans with rem_rows): loaded while the stage lands, so
     // the barrier's wait covers them; lanes past the item re-read a valid column
-    Rem32 rem;
+    constexpr bool REM = NREM > 0;
+    typename RemRegs<NREM ? NREM : 16>::V rem;
     if constexpr (REM) {
         const int sub = grp_tile_ptr[grp] + wave;
         const int subc = sub < grp_tile_ptr[grp + 1] ? sub : grp_tile_ptr[grp];
         const int sl_ = lane < rs ? lane : rs - 1;
         const int64_t cr = c0 + 2 * sl_ < p ? c0 + 2 * sl_ : c0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < (NREM ? NREM : 1); ++r) {
             const int row = rem_rows[subc * 16 + r];
             const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cr);
             rem[2 * r] = v.x;
@@ -2215,7 +2268,9 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         // every k-th column chunk's blocks entirely on the matrix cores, the other blocks walk
         // segments (no matrix-core preamble), so the two pipes are fed by different blocks
         const bool mf_item = mf_waves >= 0 || chunk % (int64_t)(-mf_waves) == 0;
-        if (mf_ptr != nullptr && mf_item) {
+        // MF: a separate instance, so the walker-only kernel keeps the walker's register count
+        // (the pipelined matrix-core path needs 91 VGPRs: two 7-wave blocks per CU instead of three)
+        if (MF && mf_ptr != nullptr && mf_item) {
             bool bad = false;
             {
                 const int nf = (grp_src_ptr[grp + 1] - grp_src_ptr[grp]) * (int)CW;
@@ -2258,7 +2313,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
                     tlds16_walk<EXACT, rs * (int)sizeof(f2)>(wacc.v[0], seg, sb0, sb1, (int)lds_base,
                                                              __float_as_int(seg_w[2 * sub]),
-                                                             __float_as_int(seg_w[2 * sub + 1]), l8w, lane);
+                                                             __float_as_int(seg_w[2 * sub + 1]), l8w, lane, 16);
 #pragma unroll
                     for (int r = 0; r < RT; ++r) {
                         const int row = __builtin_amdgcn_readlane(d_row, r);
@@ -2426,17 +2481,22 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             {                                                            // segment loop (tile.py)
                 const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
                 const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
+                // rows updated per run position: the tile's used slots rounded up to 4 / 8 / 12 / 16
+                // (wave-uniform; the slots above are unused and never stored)
+                const uint64_t used = __ballot(lane < RT && d_row >= 0);
+                const int hi = used ? 64 - __builtin_clzll(used) : 1;
+                const int nr = __builtin_amdgcn_readfirstlane(small_loops ? (hi + 3) & ~3 : 16);
                 // segment words (int4 each): a run: first slot | length << 12 | first skipped row << 20,
                 // weight-select bits, skip bits; a MASKED position: slot | 1 << 30, the rows that take
                 // it, its weight (fp32 bits).  One walker for every tile: walkers specialised by the
                 // tile's row count (4 / 8 / 12 / 16 pairs) measured no faster, and their four call
                 // sites made hipcc keep a second copy of the tuple (90 VGPRs, two blocks per CU)
                 if constexpr (REM)
-                    tlds16_walk_rem<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0,
-                                                                 w1, lane8, lane, rem);
+                    tlds16_walk_rem<EXACT, rs * (int)sizeof(f2), (NREM ? NREM : 16)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0,
+                                                                 w1, lane8, lane, nr, rem);
                 else
                     tlds16_walk<EXACT, rs * (int)sizeof(f2)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0, w1,
-                                                             lane8, lane);
+                                                             lane8, lane, nr);
                 goto tile_epilogue;
             }
         }
@@ -3478,10 +3538,12 @@ int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
 int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                              int64_t p, const niidmix_tile_lds_plan *plan, int mode, void *stream) {
     if (!plan) return set_error(NIIDMIX_EINVAL, "null plan");
-    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
     mode &= ~NIIDMIX_FLAG_AVERAGE_ONLY;
     if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
         return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (const char *e = getenv("NIIDMIX_TLDS_SMALL"))           // tuning: 0 = 16-row loop only
+        if (atoi(e) == 0) avg_only |= 2;
     if (p < 0 || plan->n_grp < 0) return set_error(NIIDMIX_EINVAL, "negative size");
     if (plan->rt != 8 && plan->rt != 16 && plan->rt != 32)
         return set_error(NIIDMIX_EUNSUPPORTED, "tile of %d rows (8, 16 or 32 supported)", plan->rt);
@@ -3522,6 +3584,9 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const bool rem = plan->rem_rows != nullptr;
     if (rem && (!seg || plan->mf_ptr != nullptr))
         return set_error(NIIDMIX_EINVAL, "rem_rows needs the segment walker (seg_ptr set, mf_ptr NULL)");
+    if (rem && plan->rem_regs != 0 && plan->rem_regs != 8 && plan->rem_regs != 16)
+        return set_error(NIIDMIX_EINVAL, "rem_regs %d (0, 8 or 16)", plan->rem_regs);
+    const bool rem8 = rem && plan->rem_regs == 8;
     if (mf && !plan->mf) return set_error(NIIDMIX_EINVAL, "null MFMA position list");
     // waves of a block on the matrix cores (the rest walk segments on the VALU side by side);
     // NIIDMIX_TLDS_MF_WAVES overrides (tuning), default every wave
@@ -3547,10 +3612,13 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
     const size_t lds = (size_t)stage_rows * cw * sizeof(float) + tlds_slack(seg, cw);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
+#define NIIDMIX_TLDS_CW(E, R, V, SG, RM, M) (cw == 120 ? k_mix_tile_lds<E, R, V, 60, SG, RM, M> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, SG, RM, M> : k_mix_tile_lds<E, R, V, 64, SG, RM, M>)
 #define NIIDMIX_TLDS(E, R, V) do { \
-        auto kfn = seg ? (rem ? (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16), (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16), (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16), (R == 16)>) \
-                              : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, (R == 16)> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, (R == 16)> : k_mix_tile_lds<E, R, V, 64, (R == 16)>)) \
-                       : (cw == 120 ? k_mix_tile_lds<E, R, V, 60, false> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, false> : k_mix_tile_lds<E, R, V, 64, false>); \
+        auto kfn = seg ? (rem ? (rem8 ? NIIDMIX_TLDS_CW(E, R, V, (R == 16), (R == 16 ? 8 : 0), false) \
+                                     : NIIDMIX_TLDS_CW(E, R, V, (R == 16), (R == 16 ? 16 : 0), false)) \
+                              : mf ? NIIDMIX_TLDS_CW(E, R, V, (R == 16), 0, (E && R == 16)) \
+                                   : NIIDMIX_TLDS_CW(E, R, V, (R == 16), 0, false)) \
+                       : NIIDMIX_TLDS_CW(E, R, V, false, 0, false); \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_tile_lds: %zu B of LDS refused", lds); \
         hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, p, (int64_t)plan->n_grp, plan->grp_tile_ptr, plan->grp_src_ptr, plan->grp_src_rows, plan->sub_ptr, plan->sub_rows, plan->sub_slot, plan->sub_wself, plan->pos_slot, plan->pos_mask, plan->pos_w, avg_only, seg ? plan->seg_ptr : nullptr, plan->seg, plan->seg_w, mf ? plan->mf_ptr : nullptr, plan->mf, mf_waves, plan->rem_rows); \
@@ -3561,6 +3629,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
 #undef NIIDMIX_TLDS_R
 #undef NIIDMIX_TLDS_V
 #undef NIIDMIX_TLDS
+#undef NIIDMIX_TLDS_CW
     return check_launch("k_mix_tile_lds");
 }
 

@@ -42,7 +42,8 @@ class TileLdsPlanC(ctypes.Structure):
                 ("sub_ptr", _vp), ("sub_rows", _vp), ("sub_slot", _vp), ("sub_wself", _vp),
                 ("pos_slot", _vp), ("pos_mask", _vp), ("pos_w", _vp), ("grp_tile_ptr", _vp),
                 ("grp_src_ptr", _vp), ("grp_src_rows", _vp), ("seg_ptr", _vp), ("seg", _vp),
-                ("seg_w", _vp), ("mf_ptr", _vp), ("mf", _vp), ("rem_rows", _vp)]
+                ("seg_w", _vp), ("mf_ptr", _vp), ("mf", _vp), ("rem_rows", _vp),
+                ("rem_regs", ctypes.c_int32)]
 
 
 class ShardC(ctypes.Structure):

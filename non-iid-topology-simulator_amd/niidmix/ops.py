@@ -323,12 +323,14 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                  max_src: int, max_tiles: int, mode: int, seg_ptr: Optional[torch.Tensor] = None,
                  seg: Optional[torch.Tensor] = None, seg_w: Optional[torch.Tensor] = None,
                  mf_ptr: Optional[torch.Tensor] = None, mf: Optional[torch.Tensor] = None,
-                 rem_rows: Optional[torch.Tensor] = None) -> None:
+                 rem_rows: Optional[torch.Tensor] = None, rem_regs: int = 16) -> None:
     """seg_ptr / seg / seg_w: the plan's segments (niidmix.tile.build_tile_segments, RT 16 only):
     the kernel's segment loop instead of the per-position loop; bit-identical results.
     mf_ptr / mf: its MFMA position lists (niidmix.tile.build_tile_mfma_positions; needs the
     segments, exact mode): the matrix-core path, bit-identical, the walker its per-block fallback.
-    rem_rows: the plan's register rows (build_tile_lds_plan(remote_regs=True); segments only)."""
+    rem_rows: the plan's register rows (build_tile_lds_plan(remote_regs=True); segments only);
+    rem_regs: how many of each tile's 16 entries the kernel loads (8 when no tile has more, else 16;
+    TileLdsPlan.rem_regs)."""
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -365,6 +367,7 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
         _req(seg_ptr is not None and mf_ptr is None,
              "register rows: with the segments and without the MFMA position lists")
         _vec("rem_rows", rem_rows, torch.int32, dev, t * 16)       # rows < x.shape[0]: the plan's
+        _req(rem_regs in (8, 16), f"rem_regs {rem_regs} (8 or 16)")
         rem = rem_rows.data_ptr()
     _no_overlap(x, out)
     some = sub_ptr.data_ptr()
@@ -372,7 +375,8 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
                              sub_rows.data_ptr(), sub_slot.data_ptr(), sub_wself.data_ptr(),
                              pos_slot.data_ptr() or some, pos_mask.data_ptr() or some,
                              pos_w.data_ptr() or some, grp_tile_ptr.data_ptr(),
-                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs, *mfs, rem)
+                             grp_src_ptr.data_ptr(), grp_src_rows.data_ptr(), *segs, *mfs, rem,
+                             int(rem_regs) if rem is not None else 0)
     rc = _lib.lib.niidmix_mix_tile_lds_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out),
                                            out.shape[0], x.shape[1], ctypes.byref(plan), int(mode),
                                            _stream(x))
@@ -629,13 +633,21 @@ class Mixer:
                 ("tlds", rt), lambda: build_tile_lds_plan(csr, grp, rt))
             # register rows for sources outside a group that only masked entries read, when the
             # stage would otherwise not fit three 120-column blocks per CU (10 000 d-cliques nodes:
-            # 199 staged rows -> 100, 128-column items); NIIDMIX_TLDS_REMOTE=0 / 1 forces it
+            # 199 staged rows -> 100, 128-column items).  At most 8 per tile when the rows past the
+            # 8th, staged, still leave three 128-column blocks per CU (80 VGPRs; 16 register rows
+            # take 96: two blocks).  NIIDMIX_TLDS_REMOTE=0 / 1 forces it off / on, 8 / 16 also the cap
             rem = os.environ.get("NIIDMIX_TLDS_REMOTE", "auto")
             lp0 = self.tlds
             if (lp0 is not None and rt == 16 and rem != "0" and
-                    (rem == "1" or (lp0.max_src + 2) * 480 + 64 > (160 * 1024) // 3)):
+                    (rem in ("1", "8", "16") or (lp0.max_src + 2) * 480 + 64 > (160 * 1024) // 3)):
                 lr, _ = self._hosted(("tlds_rem", rt),
                                      lambda: build_tile_lds_plan(csr, grp, rt, remote_regs=True))
+                if lr is not None and lr.rem_rows is not None and lr.rem_regs == 16 and rem != "16" \
+                        and (rem == "8" or self._rem8_fits(lr)):
+                    l8, _ = self._hosted(("tlds_rem8", rt), lambda: build_tile_lds_plan(
+                        csr, grp, rt, remote_regs=True, rem_cap=8))
+                    if l8 is not None and l8.rem_rows is not None:
+                        lr = l8
                 if lr is not None and lr.rem_rows is not None:
                     self.tlds = lr
         if self.tlds is None:
@@ -652,6 +664,17 @@ class Mixer:
         # unbound: `self` may be the lazy builder's scratch object, whose attribute lookups (bound
         # methods included) fall through to the Mixer
         Mixer.set_tile_lds_plan(self, lp, ts, tm)
+
+    @staticmethod
+    def _rem8_fits(lr):
+        """Would a plan with at most 8 register rows per tile (the rest staged) still stage few
+        enough rows for three 128-column blocks per CU?  Counted from the 16-row plan lr."""
+        n_reg = (lr.rem_rows.reshape(-1, 16) >= 0).sum(1)
+        extra = np.maximum(n_reg - 8, 0)
+        gtp = lr.grp_tile_ptr
+        src = np.diff(lr.grp_src_ptr)
+        most = max(int(src[g]) + int(extra[gtp[g]:gtp[g + 1]].sum()) for g in range(len(src)))
+        return (most + 2) * 512 + 1024 <= (160 * 1024) // 3
 
     def set_tile_lds_plan(self, lp, ts=None, tm=None):
         """Upload an LDS tile plan (niidmix.tile.build_tile_lds_plan), its segments (or None: the
@@ -827,7 +850,7 @@ class Mixer:
                     self.tmf is not None and self.tmf.lp is lp:
                 segs = segs + (self.m_mf_ptr, self.m_mf)
             if rem is not None:
-                segs = segs + (None, None, rem)
+                segs = segs + (None, None, rem, lp.rem_regs)
             mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
                          self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
                          self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,

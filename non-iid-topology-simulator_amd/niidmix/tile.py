@@ -260,17 +260,18 @@ class TileLdsPlan:
     max_src: int
     max_tiles: int
     rem_rows: np.ndarray = None   # int32 [T * REM_MAX] register rows per tile (-1: none), or None
+    rem_regs: int = 0             # register rows the kernel loads per tile: 8 if no tile has more, 16
 
     @property
     def n_grp(self):
         return len(self.grp_tile_ptr) - 1
 
 
-def _register_sources(tp, t0, t1, srcs, members, row_mask):
+def _register_sources(tp, t0, t1, srcs, members, row_mask, cap=None):
     """{tile: [source rows]} of a group's sources kept in REGISTERS instead of the LDS stage: a
     source outside the group (a gateway row's inter-clique neighbour) whose every position is
     taken by at most all-but-two rows of its tile -- so the segment builder can never make it part
-    of a run (runs read consecutive LDS slots) -- at most REM_MAX per tile, in list order.  At
+    of a run (runs read consecutive LDS slots) -- at most `cap` (REM_MAX) per tile, in list order.  At
     10 000 d-cliques nodes each clique reads 99 such rows, one per gateway member: staging them
     doubled the stage (199 rows), left room for 96-column items only, and each is read once."""
     rt = tp.rt
@@ -300,15 +301,18 @@ def _register_sources(tp, t0, t1, srcs, members, row_mask):
             seen[v] = seen.get(v, 0) + 1
     for t in per_tile:
         lst = [v for v in per_tile[t] if seen[v] == 1]
-        per_tile[t] = lst[:REM_MAX]
+        per_tile[t] = lst[:cap or REM_MAX]
     return per_tile
 
 
-def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False):
+def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False, rem_cap=REM_MAX):
     """(plan, None) or (None, reason): build_tile_plan over `groups`, then per group the sorted list
     of distinct source rows (every row its tiles read, self rows included) and the slot indices.
     remote_regs (RT 16, segment walker only): sources outside a group that only MASKED entries
-    read (_register_sources) are loaded into registers per tile (rem_rows) instead of staged."""
+    read (_register_sources) are loaded into registers per tile (rem_rows) instead of staged, at
+    most rem_cap (8 or 16) per tile; the rest stay staged."""
+    if rem_cap not in (8, REM_MAX):
+        raise ValueError(f"rem_cap {rem_cap} (8 or {REM_MAX})")
     if rt not in LDS_MAX_WAVES:
         return None, f"rt={rt} not in {tuple(LDS_MAX_WAVES)}"
     if groups:
@@ -355,7 +359,7 @@ def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False):
         reg_of = {}                                   # (tile, source) -> register index
         if remote:
             per_tile = _register_sources(tp, t0, t1, srcs, {int(r) for r in rows[rows >= 0]},
-                                         row_mask)
+                                         row_mask, rem_cap)
             in_regs = set()
             for t, lst in per_tile.items():
                 for i, v in enumerate(lst):
@@ -381,14 +385,19 @@ def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False):
         src_ptr.append(len(src_rows))
         max_src = max(max_src, len(srcs))
         max_tiles = max(max_tiles, t1 - t0)
+    rem_regs = 0
     if remote and not np.any(rem_rows >= 0):
         rem_rows = None                               # nothing to keep in registers
+    elif remote:
+        # 8 register rows cost 16 VGPRs fewer than 16 (k_mix_tile_lds NREM: 80 vs 96, three 7-wave
+        # blocks per CU instead of two)
+        rem_regs = 8 if not np.any(rem_rows.reshape(-1, REM_MAX)[:, 8:] >= 0) else 16
     return TileLdsPlan(tile=tp, pos_slot=pos_slot, sub_slot=sub_slot,
                        grp_tile_ptr=np.asarray(gtp, np.int32),
                        grp_src_ptr=np.asarray(src_ptr, np.int32),
                        grp_src_rows=np.asarray(src_rows, np.int32),
                        max_src=max(max_src, 1), max_tiles=max(max_tiles, 1),
-                       rem_rows=rem_rows), None
+                       rem_rows=rem_rows, rem_regs=rem_regs), None
 
 
 def apply_np(plan, x, exact=True, average_only=False):

@@ -662,14 +662,16 @@ def test_blocked_overlap_checks_use_each_block_stride(gpu):
     m.mix_blocked(x, out_ok, 2 * bc)
 
 
+@pytest.mark.parametrize("regs", [8, 16])
 @pytest.mark.parametrize("mode", ["exact", "fast"])
 @pytest.mark.parametrize("name", golden_cases("dcliques"))
-def test_tile_lds_register_rows_vs_golden(name, mode, gpu, oracle_mod, monkeypatch):
+def test_tile_lds_register_rows_vs_golden(name, mode, regs, gpu, oracle_mod, monkeypatch):
     """Plans whose out-of-group sources only masked entries read keep them in registers
-    (NIIDMIX_TLDS_REMOTE=1: build_tile_lds_plan(remote_regs=True), the 10 000-node default):
+    (NIIDMIX_TLDS_REMOTE: build_tile_lds_plan(remote_regs=True), the 10 000-node default):
     bitwise the reference in exact mode (non-finite fixtures included: inf / NaN in a gateway's
     neighbour reach the output only through the register row), within the tolerance in fast
-    mode; the stage holds fewer rows than the all-staged plan."""
+    mode; the stage holds fewer rows than the all-staged plan.  regs: the kernel with 8 register
+    rows per tile (a plan capped at 8, the rest staged) and with 16 (on the same plan)."""
     g = load_golden(name)
     if g["x"].shape[1] % 2:
         pytest.skip("odd p: the LDS tile kernel reads column pairs")
@@ -677,11 +679,13 @@ def test_tile_lds_register_rows_vs_golden(name, mode, gpu, oracle_mod, monkeypat
     m0 = _mixer(g, gpu)
     if m0.tlds is None:
         pytest.skip(m0.tlds_reason)
-    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", "1")
+    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", "8")
     m = _mixer(g, gpu)
     if m.tlds.rem_rows is None:
         pytest.skip("no source qualifies for a register row")
     assert m.tlds.max_src < m0.tlds.max_src and m.tmf is None
+    assert m.tlds.rem_regs == 8 and not (m.tlds.rem_rows.reshape(-1, 16)[:, 8:] >= 0).any()
+    m.tlds.rem_regs = regs              # 16: the 16-register kernel reads the plan's -1 entries
     x = torch.from_numpy(g["x"]).to(gpu)
     y = m(x, kernel="tile-lds-" + mode).cpu().numpy()
     if mode == "exact":

@@ -186,6 +186,43 @@ def test_segments_apply_csr_rows(name):
     _assert_rows_are_csr(tile.segments_row_lists(lp, ts), csr)
 
 
+@pytest.mark.parametrize("cap", [8, 16])
+@pytest.mark.parametrize("name", golden_cases("dcliques"))
+def test_register_rows_apply_csr_rows(name, cap):
+    """Plans with register rows (build_tile_lds_plan(remote_regs=True, rem_cap)): the walker's
+    view -- runs, masked entries, masked entries reading a register row -- still gives every row
+    its CSR row in order; at most `cap` register rows per tile, each read by one tile only, none
+    of them staged; rem_regs says how many the kernel must load."""
+    from niidmix import tile
+    g = load_golden(name)
+    csr = _csr(g)
+    lp, why = tile.build_tile_lds_plan(csr, g["cliques"], 16, remote_regs=True, rem_cap=cap)
+    if lp is None:
+        pytest.skip(why)
+    if lp.rem_rows is None:
+        pytest.skip("no source qualifies for a register row")
+    regs = lp.rem_rows.reshape(-1, tile.REM_MAX)
+    per_tile = (regs >= 0).sum(1)
+    assert per_tile.max() <= cap
+    assert lp.rem_regs == (8 if per_tile.max() <= 8 else 16)
+    gtp, gsp = lp.grp_tile_ptr, lp.grp_src_ptr
+    for gi in range(lp.n_grp):
+        in_regs = regs[gtp[gi]:gtp[gi + 1]]
+        in_regs = in_regs[in_regs >= 0]
+        assert len(np.unique(in_regs)) == len(in_regs)          # one tile, one register each
+        assert not set(in_regs.tolist()) & set(lp.grp_src_rows[gsp[gi]:gsp[gi + 1]].tolist())
+    ts = tile.build_tile_segments(lp)
+    assert ts is not None
+    _assert_rows_are_csr(tile.segments_row_lists(lp, ts), csr)
+
+
+def test_register_rows_cap_argument():
+    from niidmix import tile
+    g = load_golden("dcliques1000_fc_p64")
+    with pytest.raises(ValueError):
+        tile.build_tile_lds_plan(_csr(g), g["cliques"], 16, remote_regs=True, rem_cap=12)
+
+
 @pytest.mark.parametrize("name", golden_cases())
 def test_mfma_positions_apply_csr_rows(name):
     """The MFMA path's position lists (one entry per weight class, 4-entry groups) give every row

@@ -29,7 +29,10 @@ def main():
     ap.add_argument("--mf-items", default="",
                     help="comma list of k: also time the matrix-core path on every k-th column "
                          "chunk (NIIDMIX_TLDS_MF_WAVES=-k), the segment walker on the others")
-    ap.add_argument("--metas", default="mfma,seg,pos", help="RT 16 variants to time")
+    ap.add_argument("--metas", default="mfma,seg,pos",
+                    help="RT 16 variants to time: mfma, seg (segment walker), seg16 (walker without "
+                         "its 8- / 4-row loops, NIIDMIX_TLDS_SMALL=0), pos (per-position loop), "
+                         "rem8 / rem16 (walker with register rows, 8 / 16 per tile)")
     ap.add_argument("--lds-rows", type=int, default=0,
                     help="occupancy probe: reserve LDS for this many staged rows (max_src) per block")
     a = ap.parse_args()
@@ -45,6 +48,7 @@ def main():
         csr = csr.relabel(perm)
         cliques = [[int(perm[r]) for r in c] for c in cliques]
     mixers = {}
+    rem_mixer, rem_natural = None, 16
     for rt in a.rts.split(","):
         os.environ["NIIDMIX_TILE_LDS_RT"] = rt
         m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
@@ -52,6 +56,14 @@ def main():
         if a.lds_rows:
             m.tlds.max_src = max(m.tlds.max_src, a.lds_rows)
         mixers[int(rt)] = m
+        if rt == "16" and any(k.startswith("rem") for k in a.metas.split(",")):
+            os.environ["NIIDMIX_TLDS_REMOTE"] = "1"
+            mr = ops.Mixer(csr=csr, cliques=cliques, device=dev)
+            assert mr.tlds is not None and mr.tlds.rem_rows is not None, mr.tlds_reason
+            os.environ.pop("NIIDMIX_TLDS_REMOTE")
+            print(f"register-row plan: {mr.tlds.max_src} staged rows (all staged: {m.tlds.max_src}), "
+                  f"rem_regs {mr.tlds.rem_regs}", flush=True)
+            rem_mixer, rem_natural = mr, mr.tlds.rem_regs
     n = csr.n
     x = memory.empty_slab(n, a.p, dev)
     x.normal_(generator=torch.Generator(device=dev).manual_seed(0))
@@ -62,12 +74,23 @@ def main():
         for rt, m in mixers.items():
             metas = a.metas.split(",") + [f"mfitem{k}" for k in a.mf_items.split(",") if k]
             for meta in (metas if rt == 16 else ("pos",)):
+                if meta.startswith("rem"):
+                    m = rem_mixer
+                    if int(meta[3:]) < rem_natural:
+                        continue                          # the plan has tiles with more rows
+                    m.tlds.rem_regs = int(meta[3:])      # 16: the 16-register kernel on the same plan
+                else:
+                    m = mixers[rt]
                 m.use_segments = meta != "pos"
                 m.use_mfma = meta.startswith("mf")
                 if meta.startswith("mfitem"):
                     os.environ["NIIDMIX_TLDS_MF_WAVES"] = "-" + meta[6:]
                 else:
                     os.environ.pop("NIIDMIX_TLDS_MF_WAVES", None)
+                if meta == "seg16":
+                    os.environ["NIIDMIX_TLDS_SMALL"] = "0"
+                else:
+                    os.environ.pop("NIIDMIX_TLDS_SMALL", None)
                 m(x, out=y, kernel="tile-lds-exact")
                 torch.cuda.synchronize()
                 if ref is None:
