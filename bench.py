@@ -196,15 +196,20 @@ def cold_cache_rounds(step, xa, xb, dev, rounds=10, flush_bytes=1 << 30):
     between graph-replayed rounds) is also timed once cold.  Before each round a 1 GiB scratch
     buffer is read and written (evicting the MALL and every XCD's L2), then ONE round is timed
     alone with HIP events on the launch stream; the same single-round timing without the flush is
-    reported beside it (eager launches, so both include one launch's overhead, unlike the graph)."""
+    reported beside it (eager launches, so both include one launch's gap, unlike the graph).  The
+    GPU is kept busy while the round is enqueued (the flush, or a short spin for the warm round), so
+    the events time the GPU's work, not the host's enqueue of it."""
     scratch = torch.zeros(flush_bytes // 4, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    spin = getattr(torch.cuda, "_sleep", None)
     res = {}
     for name, flush in (("warm_eager_us", False), ("cold_us", True)):
         ts = []
         for _ in range(rounds):
             if flush:
                 scratch.add_(1.0)
+            elif spin is not None:
+                spin(1 << 20)                           # ~0.5 ms of GPU spin, touches no memory
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             step(xa, xb)

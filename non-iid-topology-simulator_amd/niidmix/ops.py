@@ -631,15 +631,17 @@ class Mixer:
                 grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
             self.tlds, self.tlds_reason = self._hosted(
                 ("tlds", rt), lambda: build_tile_lds_plan(csr, grp, rt))
-            # register rows for sources outside a group that only masked entries read, when the
-            # stage would otherwise not fit three 120-column blocks per CU (10 000 d-cliques nodes:
-            # 199 staged rows -> 100, 128-column items).  At most 8 per tile when the rows past the
-            # 8th, staged, still leave three 128-column blocks per CU (80 VGPRs; 16 register rows
-            # take 96: two blocks).  NIIDMIX_TLDS_REMOTE=0 / 1 forces it off / on, 8 / 16 also the cap
+            # register rows for sources outside a group that only masked entries read (a gateway
+            # row's inter-clique neighbour): the stage shrinks to the group's own rows (10 000
+            # d-cliques nodes: 199 staged rows -> 100, 128-column items instead of 96; 1000 nodes:
+            # 111 -> 101, 128 instead of 120).  At most 8 per tile when the rows past the 8th,
+            # staged, still leave three 128-column blocks per CU (80 VGPRs; 16 register rows take
+            # 96: two blocks).  Same-box A/B, 1000 nodes: 2.92 (8) / 3.03 (16) vs 3.11 ms all
+            # staged (profiles/r04/exact_register_rows_ab.txt).  NIIDMIX_TLDS_REMOTE=0 turns it
+            # off; 8 / 16 fix the cap
             rem = os.environ.get("NIIDMIX_TLDS_REMOTE", "auto")
             lp0 = self.tlds
-            if (lp0 is not None and rt == 16 and rem != "0" and
-                    (rem in ("1", "8", "16") or (lp0.max_src + 2) * 480 + 64 > (160 * 1024) // 3)):
+            if lp0 is not None and rt == 16 and rem != "0":
                 lr, _ = self._hosted(("tlds_rem", rt),
                                      lambda: build_tile_lds_plan(csr, grp, rt, remote_regs=True))
                 if lr is not None and lr.rem_rows is not None and lr.rem_regs == 16 and rem != "16" \

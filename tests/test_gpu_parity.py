@@ -268,15 +268,24 @@ def test_tile_lds_segment_loop_masked_heavy(n, size, inter, gpu, oracle_mod):
     assert oracle_mod.bitwise_equal(y, ref), (n, size, inter)
 
 
-def test_tile_lds_narrow_items_float2(gpu, oracle_mod):
-    """The 1000-node d-cliques plan picks 120-column items by itself (109 staged rows); p = 1002
+@pytest.mark.parametrize("remote", ["0", "auto"])
+def test_tile_lds_narrow_items_float2(remote, gpu, oracle_mod, monkeypatch):
+    """The all-staged 1000-node d-cliques plan picks 120-column items by itself (109 staged
+    rows); the default plan (8 register rows per tile, 101 staged) 128-column items; p = 1002
     (p % 4 == 2: float2 staging) ends in a ragged item.  Bitwise against the C oracle."""
+    monkeypatch.setenv("NIIDMIX_TLDS_REMOTE", remote)
     g = load_golden("dcliques1000_fc_p64")
     x = np.random.default_rng(5).standard_normal((g["x"].shape[0], 1002)).astype(np.float32)
     x[3, 7] = -0.0
     x[11, 1001] = np.float32(1e-42)
-    m = _tile_lds_mixer(g, gpu, 16)
-    assert m.tlds.max_src * 128 * 4 > 160 * 1024 // 3 >= m.tlds.max_src * 120 * 4
+    m = _mixer(g, gpu)                  # the Mixer's own plan choice (RT 16, segments)
+    assert m.tlds is not None and m.tlds.tile.rt == 16 and m.tseg is not None
+    if remote == "0":
+        assert m.tlds.rem_rows is None
+        assert m.tlds.max_src * 128 * 4 > 160 * 1024 // 3 >= m.tlds.max_src * 120 * 4
+    else:
+        assert m.tlds.rem_rows is not None and m.tlds.rem_regs == 8
+        assert (m.tlds.max_src + 2) * 128 * 4 + 1024 <= 160 * 1024 // 3
     y = m(torch.from_numpy(x).to(gpu), kernel="tile-lds-exact").cpu().numpy()
     ref = oracle_mod.mix_exact_c(x, g["row_ptr"], g["col"], g["val"])
     assert oracle_mod.bitwise_equal(y, ref)
