@@ -2246,10 +2246,12 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const int64_t cr = c0 + 2 * sl_ < p ? c0 + 2 * sl_ : c0;
 #pragma unroll
         for (int r = 0; r < (NREM ? NREM : 1); ++r) {
-            const int row = rem_rows[subc * 16 + r];
-            const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cr);
-            rem[2 * r] = v.x;
-            rem[2 * r + 1] = v.y;
+            const int row = rem_rows[subc * 16 + r];             // wave-uniform; -1: unused (never
+            if (row >= 0) {                                      // read by the walker), not loaded
+                const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)row * ld_x + cr);
+                rem[2 * r] = v.x;
+                rem[2 * r + 1] = v.y;
+            }
         }
     }
     __syncthreads();
