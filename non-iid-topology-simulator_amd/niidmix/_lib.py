@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must be loaded before libniidmix.so, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NIIDMIX_LIB", os.path.join(_HERE, "libniidmix.so"))
+LIB_PATH = os.environ.get("NIIDMIX_LIB") or os.path.join(_HERE, "libniidmix.so")
 
 OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
 MODE_EXACT, MODE_FAST = 0, 1
