@@ -18,9 +18,9 @@ cat $O/bench_headline_default.json
 one() {   # name kernel-substring alg-bytes bench-args...
   n=$1; k=$2; alg=$3; shift 3
   timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench $n failed"; tail -5 $O/bench_$n.err; return 1; }
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt_$n -o kt -- python3 $R/bench.py --no-cpu-baseline "$@" > $O/kt_$n.log 2>&1 || { echo "trace $n failed"; tail -5 $O/kt_$n.log; return 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt_$n -o kt -- python3 $R/bench.py --no-cpu-baseline --no-cold-cache "$@" > $O/kt_$n.log 2>&1 || { echo "trace $n failed"; tail -5 $O/kt_$n.log; return 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/$O/pmc_${n}_$c -o p -- python3 $R/bench.py --no-cpu-baseline "$@" > $O/pmc_${n}_$c.log 2>&1 || { echo "pmc $n $c failed"; tail -5 $O/pmc_${n}_$c.log; return 1; }
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/$O/pmc_${n}_$c -o p -- python3 $R/bench.py --no-cpu-baseline --no-cold-cache "$@" > $O/pmc_${n}_$c.log 2>&1 || { echo "pmc $n $c failed"; tail -5 $O/pmc_${n}_$c.log; return 1; }
   done
   python tools/pmc_traffic.py $O/pmc_${n}_FETCH_SIZE $O/pmc_${n}_WRITE_SIZE $k --alg-bytes $alg --key-from $O/bench_$n.json --out $O/traffic.json > $O/traffic_$n.txt || return 1
   python -c "import json;d=json.load(open('$O/bench_$n.json'));t=json.load(open('$O/traffic_$n.txt'));print('$n', d['ms_per_step'], 'ms', d['roofline']['frac'], 'traffic x', round(t['ratio_to_algorithmic'],4))"
@@ -29,6 +29,7 @@ one headline k_mix_clique 8388608000 --steps 20 || exit 5
 one exact k_mix_tile_lds 8388608000 --kernel tile-lds-exact --steps 10 || exit 5
 one fc1000 k_mix_bigclique 8388608000 --config fc1000 --steps 10 || exit 5
 one d10k k_mix_clique 83886080000 --config dcliques10000 --steps 5 --warmup 2 || exit 5
+one d10k_exact k_mix_tile_lds 83886080000 --config dcliques10000 --kernel tile-lds-exact --steps 3 --warmup 1 || exit 5
 one ring100 k_mix_band 49604800 --config ring100 --steps 200 || exit 5
 one grad k_grad_segment_mean 8388608000 --workload grad-clique --steps 10 || exit 5
 one dense k_mix_dense 8388608000 --config fc1000 --kernel dense --steps 3 --warmup 1 || exit 5
