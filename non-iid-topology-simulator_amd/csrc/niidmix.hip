@@ -2131,6 +2131,8 @@ inline size_t tlds_slack(bool seg, int cw) {
 }
 constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
 
+template <bool B> struct BoolC { static constexpr bool value = B; };
+
 template <bool EXACT, int RT, int SV, int RS, bool SEG, int NREM = 0, bool MF = false>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
@@ -2181,6 +2183,38 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             typedef __attribute__((address_space(1))) void glb_void;
             constexpr int NB = 8;
             const int step = n_waves * kWave;
+            if constexpr (kWave % PPR == 0) {
+                // a wave-instruction's 64 pieces are kWave / PPR whole rows (128-column items:
+                // two), so a lane's piece -- its column offset -- is the same in every one: the
+                // per-DMA address is one 32 x 32 -> 64-bit multiply-add on the row index (the
+                // general form below spends ~23 VALU per DMA on divisions and 64-bit clamps)
+                const int piece = lane % PPR;
+                const int64_t cl = c0 + (int64_t)piece * 4;
+                const uint64_t xl = reinterpret_cast<uint64_t>(x + (cl < p ? cl : c0));
+                const uint32_t ldx4 = (uint32_t)ld_x * 4u;      // row pitch in bytes < 2^32
+                                                                // (launcher: ld_x < 2^30)
+                for (int b0 = wave * kWave; b0 < total; b0 += NB * step) {
+                    int rowi[NB];
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        const int slot = (b0 + u * step) / PPR + lane / PPR;   // rows past the
+                        rowi[u] = grp_src_rows[s0 + (slot < ns ? slot : ns - 1)]; // stage: any
+                    }
+                    uint64_t src[NB];
+#pragma unroll
+                    for (int u = 0; u < NB; ++u)
+                        src[u] = xl + (uint64_t)(uint32_t)rowi[u] * ldx4;   // v_mad_u64_u32
+                    asm volatile("" ::"v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3]), "v"(src[4]),
+                                 "v"(src[5]), "v"(src[6]), "v"(src[7]));
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        const int i0 = b0 + u * step;
+                        if (i0 < total)
+                            __builtin_amdgcn_global_load_lds(reinterpret_cast<glb_void *>(src[u]),
+                                                             (lds_void *)(st + 4 * i0), 16, 0, 0);
+                    }
+                }
+            } else
             for (int b0 = wave * kWave; b0 < total; b0 += NB * step) {
                 int rowi[NB];
 #pragma unroll
@@ -2246,12 +2280,13 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const int64_t cr = c0 + 2 * sl_ < p ? c0 + 2 * sl_ : c0;
 #pragma unroll
         for (int r = 0; r < (NREM ? NREM : 1); ++r) {
-            const int row = rem_rows[subc * 16 + r];             // wave-uniform; -1: unused (never
-            if (row >= 0) {                                      // read by the walker), not loaded
-                const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)row * ld_x + cr);
-                rem[2 * r] = v.x;
-                rem[2 * r + 1] = v.y;
-            }
+            // -1 (unused, never read by the walker) loads row 0: skipping the load instead (a
+            // branch per slot) cost 21 more VGPRs for 8 register rows and spilled the 16-row kernel
+            // to scratch (2.95 -> 3.46 / 3.07 -> 12.7 ms)
+            const int row = rem_rows[subc * 16 + r];
+            const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cr);
+            rem[2 * r] = v.x;
+            rem[2 * r + 1] = v.y;
         }
     }
     __syncthreads();
@@ -2681,24 +2716,31 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         // update_models: z + acc, z = x_self*0 (AVERAGE_ONLY: acc).  Four rows at a time: their
         // own staged values are read together (an unused slot reads slot 0), then combined and
         // stored, so the LDS latency is paid once per four rows instead of once per row
+        // (avg_only is tested once, not per row: per row it became two v_cndmask per row)
+        auto epilogue = [&](auto with_z) {
 #pragma unroll
-        for (int r0 = 0; r0 < RT; r0 += 4) {
-            f2 xs[4];
+            for (int r0 = 0; r0 < RT; r0 += 4) {
+                f2 xs[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) xs[u] = stage[__builtin_amdgcn_readlane(d_slot, r0 + u) * rs + sl];
+                for (int u = 0; u < 4; ++u) xs[u] = stage[sub_slot[sub * RT + r0 + u] * rs + sl];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int row = __builtin_amdgcn_readlane(d_row, r0 + u);
-                if (row < 0) continue;                              // wave-uniform
-                f2 o = acc.get(r0 + u);
-                if (!avg_only) o = xs[u] * 0.f + o;
-                if (ok) {
-                    float *dst = y + (int64_t)row * ld_y + col;
-                    __builtin_nontemporal_store(o.x, dst);
-                    __builtin_nontemporal_store(o.y, dst + 1);
+                for (int u = 0; u < 4; ++u) {
+                    const int row = sub_rows[sub * RT + r0 + u];    // scalar loads, not v_readlane
+                    if (row < 0) continue;                          // wave-uniform
+                    f2 o = acc.get(r0 + u);
+                    if constexpr (decltype(with_z)::value) o = xs[u] * 0.f + o;
+                    if (ok) {
+                        float *dst = y + (int64_t)row * ld_y + col;
+                        __builtin_nontemporal_store(o.x, dst);
+                        __builtin_nontemporal_store(o.y, dst + 1);
+                    }
                 }
             }
-        }
+        };
+        if (avg_only)
+            epilogue(BoolC<false>{});
+        else
+            epilogue(BoolC<true>{});
     }
 }
 
@@ -3555,6 +3597,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
         !plan->pos_slot || !plan->pos_mask || !plan->pos_w)
         return set_error(NIIDMIX_EINVAL, "null pointer");
     if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (ld_x >= (1LL << 30)) return set_error(NIIDMIX_EUNSUPPORTED, "ld_x >= 2^30");
     if (n_rows < 1) return set_error(NIIDMIX_EINVAL, "n_rows < 1");
     if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
