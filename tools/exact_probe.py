@@ -51,8 +51,10 @@ def main():
     rem_mixer, rem_natural = None, 16
     for rt in a.rts.split(","):
         os.environ["NIIDMIX_TILE_LDS_RT"] = rt
+        os.environ["NIIDMIX_TLDS_REMOTE"] = "0"          # all staged; rem8 / rem16 below
         m = ops.Mixer(csr=csr, cliques=cliques, device=dev)
         assert m.tlds is not None, m.tlds_reason
+        os.environ.pop("NIIDMIX_TLDS_REMOTE")
         if a.lds_rows:
             m.tlds.max_src = max(m.tlds.max_src, a.lds_rows)
         mixers[int(rt)] = m
