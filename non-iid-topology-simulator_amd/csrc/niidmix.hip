@@ -1989,100 +1989,85 @@ __device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp,
 // v[0:31] until the walker and was copied into v[32:63] there: 32 extra VGPRs at the peak (90, so
 // only two 7-wave blocks per CU instead of the three the LDS allows).  Rows' LDS reads two ahead.
 template <bool EXACT>
-__device__ __forceinline__ void tlds16_init(Acc16 &acc, const int32_t *slots, const float *wself, int rb,
-                                            int base, int lane8) {
-    // slots / wself: the tile's 16 LDS slots and self weights, read by two scalar loads (16
-    // v_readlane each before: 32 of the wave's ~2000 VALU instructions)
+__device__ __forceinline__ void tlds16_init(Acc16 &acc, int d_slot, int d_ws, int rb, int base, int lane8) {
     uint64_t x0, x1, t, pr;
     uint32_t va;
     if constexpr (EXACT)
-        asm volatile("s_load_dwordx16 s[48:63], %[sp], 0\n\t"
-                 "s_load_dwordx16 s[64:79], %[wp], 0\n\t"
-                 "s_mov_b64 s[46:47], 0\n\t"
-                 "s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mul_i32 s40, s48, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mul_i32 s40, s49, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[64:65] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[32:33], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s50, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s65\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[34:35], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s51, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[66:67] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[36:37], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s52, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s67\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[38:39], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s53, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[68:69] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[40:41], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s54, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s69\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[42:43], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s55, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[70:71] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[44:45], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s56, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s71\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[46:47], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s57, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[72:73] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[48:49], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s58, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s73\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[50:51], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s59, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[74:75] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[52:53], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s60, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s75\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[54:55], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s61, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[76:77] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[56:57], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s62, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s77\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[58:59], %[t], %[pr]\n\t"
-                 "s_mul_i32 s40, s63, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[78:79] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[60:61], %[t], %[pr]\n\t"
-                 "s_mov_b32 s42, s79\n\t""s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[62:63], %[t], %[pr]\n\t"
+        asm volatile("s_mov_b64 s[46:47], 0\n\t"
+                 "v_readlane_b32 s40, %[ds], 0\n\t""v_readlane_b32 s42, %[dw], 0\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "v_readlane_b32 s40, %[ds], 1\n\t""v_readlane_b32 s44, %[dw], 1\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[32:33], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 2\n\t""v_readlane_b32 s42, %[dw], 2\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[34:35], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 3\n\t""v_readlane_b32 s44, %[dw], 3\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[36:37], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 4\n\t""v_readlane_b32 s42, %[dw], 4\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[38:39], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 5\n\t""v_readlane_b32 s44, %[dw], 5\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[40:41], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 6\n\t""v_readlane_b32 s42, %[dw], 6\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[42:43], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 7\n\t""v_readlane_b32 s44, %[dw], 7\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[44:45], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 8\n\t""v_readlane_b32 s42, %[dw], 8\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[46:47], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 9\n\t""v_readlane_b32 s44, %[dw], 9\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[48:49], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 10\n\t""v_readlane_b32 s42, %[dw], 10\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[50:51], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 11\n\t""v_readlane_b32 s44, %[dw], 11\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[52:53], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 12\n\t""v_readlane_b32 s42, %[dw], 12\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[54:55], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 13\n\t""v_readlane_b32 s44, %[dw], 13\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[56:57], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 14\n\t""v_readlane_b32 s42, %[dw], 14\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[58:59], %[t], %[pr]\n\t"
+                 "v_readlane_b32 s40, %[ds], 15\n\t""v_readlane_b32 s44, %[dw], 15\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x0], s[42:43] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[60:61], %[t], %[pr]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_mul_f32 %[pr], %[x1], s[44:45] op_sel_hi:[1,0]\n\t""v_pk_add_f32 v[62:63], %[t], %[pr]\n\t"
                  : "={v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [t] "=&v"(t), [pr] "=&v"(pr),
                    [va] "=&v"(va)
-                 : [sp] "s"(slots), [wp] "s"(wself), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
-                 : "s40", "s42", "s43", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54",
-                   "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
-                   "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78",
-                   "s79", "memory");
+                 : [ds] "v"(d_slot), [dw] "v"(d_ws), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
+                 : "s40", "s42", "s43", "s44", "s45", "s46", "s47", "memory");
     else
-        asm volatile("s_load_dwordx16 s[48:63], %[sp], 0\n\t"
-                 "s_load_dwordx16 s[64:79], %[wp], 0\n\t"
-                 "s_mov_b64 s[46:47], 0\n\t"
-                 "s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mul_i32 s40, s48, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mul_i32 s40, s49, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[32:33], %[x0], s[64:65], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s50, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s65\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[34:35], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s51, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[36:37], %[x0], s[66:67], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s52, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s67\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[38:39], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s53, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[40:41], %[x0], s[68:69], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s54, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s69\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[42:43], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s55, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[44:45], %[x0], s[70:71], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s56, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s71\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[46:47], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s57, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[48:49], %[x0], s[72:73], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s58, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s73\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[50:51], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s59, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[52:53], %[x0], s[74:75], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s60, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s75\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[54:55], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s61, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[56:57], %[x0], s[76:77], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s62, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
-                 "s_mov_b32 s42, s77\n\t""s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[58:59], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mul_i32 s40, s63, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
-                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[60:61], %[x0], s[78:79], %[t] op_sel_hi:[1,0,1]\n\t"
-                 "s_mov_b32 s42, s79\n\t""s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[62:63], %[x1], s[42:43], %[t] op_sel_hi:[1,0,1]\n\t"
+        asm volatile("s_mov_b64 s[46:47], 0\n\t"
+                 "v_readlane_b32 s40, %[ds], 0\n\t""v_readlane_b32 s42, %[dw], 0\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "v_readlane_b32 s40, %[ds], 1\n\t""v_readlane_b32 s44, %[dw], 1\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[32:33], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 2\n\t""v_readlane_b32 s42, %[dw], 2\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[34:35], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 3\n\t""v_readlane_b32 s44, %[dw], 3\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[36:37], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 4\n\t""v_readlane_b32 s42, %[dw], 4\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[38:39], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 5\n\t""v_readlane_b32 s44, %[dw], 5\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[40:41], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 6\n\t""v_readlane_b32 s42, %[dw], 6\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[42:43], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 7\n\t""v_readlane_b32 s44, %[dw], 7\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[44:45], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 8\n\t""v_readlane_b32 s42, %[dw], 8\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[46:47], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 9\n\t""v_readlane_b32 s44, %[dw], 9\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[48:49], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 10\n\t""v_readlane_b32 s42, %[dw], 10\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[50:51], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 11\n\t""v_readlane_b32 s44, %[dw], 11\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[52:53], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 12\n\t""v_readlane_b32 s42, %[dw], 12\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[54:55], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 13\n\t""v_readlane_b32 s44, %[dw], 13\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[56:57], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 14\n\t""v_readlane_b32 s42, %[dw], 14\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x0], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[58:59], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "v_readlane_b32 s40, %[ds], 15\n\t""v_readlane_b32 s44, %[dw], 15\n\t""s_mul_i32 s40, s40, %[rb]\n\t""s_add_u32 s40, s40, %[base]\n\t""v_add_u32 %[va], s40, %[l8]\n\t""ds_read_b64 %[x1], %[va]\n\t"
+                 "s_waitcnt lgkmcnt(1)\n\t""v_pk_mul_f32 %[t], %[x0], s[46:47]\n\t""v_pk_fma_f32 v[60:61], %[x0], s[42:43] , %[t] op_sel_hi:[1,0,1]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t""v_pk_mul_f32 %[t], %[x1], s[46:47]\n\t""v_pk_fma_f32 v[62:63], %[x1], s[44:45] , %[t] op_sel_hi:[1,0,1]\n\t"
                  : "={v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [t] "=&v"(t), [pr] "=&v"(pr),
                    [va] "=&v"(va)
-                 : [sp] "s"(slots), [wp] "s"(wself), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
-                 : "s40", "s42", "s43", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54",
-                   "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
-                   "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78",
-                   "s79", "memory");
+                 : [ds] "v"(d_slot), [dw] "v"(d_ws), [rb] "s"(rb), [base] "s"(base), [l8] "v"(lane8)
+                 : "s40", "s42", "s43", "s44", "s45", "s46", "s47", "memory");
     (void)pr;
 }
 
@@ -2360,7 +2345,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                     const unsigned lds_base = (unsigned)(size_t)(lds_float_w *)lds_tile;
                     TileAcc<16> wacc;
                     const int l8w = slw * (int)sizeof(f2);
-                    tlds16_init<EXACT>(wacc.v[0], sub_slot + sub * RT, sub_wself + sub * RT, rs * (int)sizeof(f2),
+                    tlds16_init<EXACT>(wacc.v[0], d_slot, __float_as_int(d_ws), rs * (int)sizeof(f2),
                                        (int)lds_base, l8w);
                     const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
                     tlds16_walk<EXACT, rs * (int)sizeof(f2)>(wacc.v[0], seg, sb0, sb1, (int)lds_base,
@@ -2520,8 +2505,7 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
         const float d_ws = sub_wself[sub * RT + li];
         TileAcc<RT> acc;
         if constexpr (SEG && RT == 16 && NIIDMIX_TLDS_ASM && (NIIDMIX_TLDS_SPLIT == 0 || NIIDMIX_TLDS_SPLIT == 2)) {
-            tlds16_init<EXACT>(acc.v[0], sub_slot + sub * RT, sub_wself + sub * RT, rs * (int)sizeof(f2),
-                               (int)lds_base, lane8);
+            tlds16_init<EXACT>(acc.v[0], d_slot, __float_as_int(d_ws), rs * (int)sizeof(f2), (int)lds_base, lane8);
         } else {
 #pragma unroll
             for (int r = 0; r < RT; ++r) {
