@@ -1772,7 +1772,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // the remaining rows), s43 dz, s44 weight, s46 skipped row * 2 / row index, s47 position.  VGPR
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
 // saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
-#define NIIDMIX_SEG_UPD_EXACT(XD, W) "v_pk_mul_f32 %[pr], " XD ", " W " op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
 // the same for tiles whose rows all sit in the first 12 / 8 / 4 slots (a 1000-node d-clique's 9
 // gateway rows form their own tile: 12 adds per position instead of 16)
 #define NIIDMIX_ADD4(T)                                                                             \
@@ -1786,43 +1786,35 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     NIIDMIX_ADD8(T)                                                                                 \
     "v_pk_add_f32 v[48:49], v[48:49], " T "\n\tv_pk_add_f32 v[50:51], v[50:51], " T "\n\t"          \
     "v_pk_add_f32 v[52:53], v[52:53], " T "\n\tv_pk_add_f32 v[54:55], v[54:55], " T "\n\t"
-#define NIIDMIX_SEG_UPD_EXACT12(XD, W) "v_pk_mul_f32 %[pr], " XD ", " W " op_sel_hi:[1,0]\n\t" NIIDMIX_ADD12("%[pr]")
-#define NIIDMIX_SEG_UPD_EXACT8(XD, W) "v_pk_mul_f32 %[pr], " XD ", " W " op_sel_hi:[1,0]\n\t" NIIDMIX_ADD8("%[pr]")
-#define NIIDMIX_SEG_UPD_EXACT4(XD, W) "v_pk_mul_f32 %[pr], " XD ", " W " op_sel_hi:[1,0]\n\t" NIIDMIX_ADD4("%[pr]")
-// fast mode: one fma per row with the position's weight pair W
-#define NIIDMIX_SFMA(R, XD, W) "v_pk_fma_f32 " R ", " XD ", " W ", " R " op_sel_hi:[1,0,1]\n\t"
-#define NIIDMIX_SEG_UPD_FAST4(XD, W)                                                                \
-    NIIDMIX_SFMA("v[32:33]", XD, W) NIIDMIX_SFMA("v[34:35]", XD, W) NIIDMIX_SFMA("v[36:37]", XD, W)   \
-    NIIDMIX_SFMA("v[38:39]", XD, W)
-#define NIIDMIX_SEG_UPD_FAST8(XD, W)                                                                \
-    NIIDMIX_SEG_UPD_FAST4(XD, W) NIIDMIX_SFMA("v[40:41]", XD, W) NIIDMIX_SFMA("v[42:43]", XD, W)      \
-    NIIDMIX_SFMA("v[44:45]", XD, W) NIIDMIX_SFMA("v[46:47]", XD, W)
-#define NIIDMIX_SEG_UPD_FAST12(XD, W)                                                               \
-    NIIDMIX_SEG_UPD_FAST8(XD, W) NIIDMIX_SFMA("v[48:49]", XD, W) NIIDMIX_SFMA("v[50:51]", XD, W)      \
-    NIIDMIX_SFMA("v[52:53]", XD, W) NIIDMIX_SFMA("v[54:55]", XD, W)
-#define NIIDMIX_SEG_UPD_FAST(XD, W)                                                                 \
-    NIIDMIX_SEG_UPD_FAST12(XD, W) NIIDMIX_SFMA("v[56:57]", XD, W) NIIDMIX_SFMA("v[58:59]", XD, W)     \
-    NIIDMIX_SFMA("v[60:61]", XD, W) NIIDMIX_SFMA("v[62:63]", XD, W)
-// Position k of the unrolled loop applies weight pair W (written two positions earlier: an SGPR that
-// a SALU op has just written stalls the VALU op reading it) and selects the weight of position
-// k + 2 into WN from s57 = the weight-select bits >> 2.
-#define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD, W, WN)                                                  \
+#define NIIDMIX_SEG_UPD_EXACT12(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD12("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT8(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD8("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT4(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD4("%[pr]")
+#define NIIDMIX_UPD_FAST4(XD)                                                                       \
+    NIIDMIX_FMA1("v[32:33]", XD) NIIDMIX_FMA1("v[34:35]", XD) NIIDMIX_FMA1("v[36:37]", XD)            \
+    NIIDMIX_FMA1("v[38:39]", XD)
+#define NIIDMIX_UPD_FAST8(XD)                                                                       \
+    NIIDMIX_UPD_FAST4(XD) NIIDMIX_FMA1("v[40:41]", XD) NIIDMIX_FMA1("v[42:43]", XD)                 \
+    NIIDMIX_FMA1("v[44:45]", XD) NIIDMIX_FMA1("v[46:47]", XD)
+#define NIIDMIX_UPD_FAST12(XD)                                                                      \
+    NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMA1("v[48:49]", XD) NIIDMIX_FMA1("v[50:51]", XD)                 \
+    NIIDMIX_FMA1("v[52:53]", XD) NIIDMIX_FMA1("v[54:55]", XD)
+#define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
-    "s_bitcmp1_b32 s57, s47\n\t"                                                                     \
-    "s_cselect_b32 " WN ", %[w1], %[w0]\n\t"                                                         \
+    "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
+    "s_cselect_b32 s44, %[w1], %[w0]\n\t"                                                            \
     "s_bitcmp1_b32 s43, s47\n\t"                                                                     \
     "s_waitcnt lgkmcnt(2)\n\t"                                                                       \
-    "s_cbranch_scc1 .Lseg_skip" K "_%=\n\t" UPD(XD, W)                                              \
+    "s_cbranch_scc1 .Lseg_skip" K "_%=\n\t" UPD(XD)                                                 \
     "\n.Lseg_back" K "_%=:\n\t"                                                                     \
     "s_add_u32 s47, s47, 1\n\t"                                                                      \
     "s_cmp_ge_u32 s47, s38\n\t"                                                                      \
     "s_cbranch_scc1 .Lw_next_%=\n\t"
-#define NIIDMIX_SEG_SKIPBLK(XD, K, UPD, W)                                                           \
+#define NIIDMIX_SEG_SKIPBLK(XD, K, UPD)                                                              \
     "\n.Lseg_skip" K "_%=:\n\t"                                                                     \
     "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
     "v_mov_b32 %[sv0], v32\n\t"                                                                      \
     "v_mov_b32 %[sv1], v33\n\t"                                                                      \
-    "s_set_gpr_idx_off\n\t" UPD(XD, W)                                                               \
+    "s_set_gpr_idx_off\n\t" UPD(XD)                                                                  \
     "s_set_gpr_idx_on s46, gpr_idx(DST)\n\t"                                                        \
     "v_mov_b32 v32, %[sv0]\n\t"                                                                      \
     "v_mov_b32 v33, %[sv1]\n\t"                                                                      \
@@ -1877,16 +1869,16 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // first nr slots); the 12-, 8- and 4-row loops are copies of the 16-row one with fewer adds
 #define NIIDMIX_SEG_LOOP(S, UPD)                                                                     \
     ".Lseg_loop" S "_%=:\n\t"                                                                       \
-    NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", S "0", UPD, "s[48:49]", "s52")                           \
-    NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", S "1", UPD, "s[50:51]", "s54")                           \
-    NIIDMIX_SEG_POS("%[x2]", "%[x0]", "o4", S "2", UPD, "s[52:53]", "s48")                           \
-    NIIDMIX_SEG_POS("%[x3]", "%[x1]", "o5", S "3", UPD, "s[54:55]", "s50")                           \
+    NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", S "0", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x1]", "%[x3]", "o3", S "1", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x2]", "%[x0]", "o4", S "2", UPD)                                              \
+    NIIDMIX_SEG_POS("%[x3]", "%[x1]", "o5", S "3", UPD)                                              \
     "v_add_u32 %[va], %[o4], %[va]\n\t"                                                             \
     "s_branch .Lseg_loop" S "_%=\n\t"                                                               \
-    NIIDMIX_SEG_SKIPBLK("%[x0]", S "0", UPD, "s[48:49]")                                             \
-    NIIDMIX_SEG_SKIPBLK("%[x1]", S "1", UPD, "s[50:51]")                                             \
-    NIIDMIX_SEG_SKIPBLK("%[x2]", S "2", UPD, "s[52:53]")                                             \
-    NIIDMIX_SEG_SKIPBLK("%[x3]", S "3", UPD, "s[54:55]")
+    NIIDMIX_SEG_SKIPBLK("%[x0]", S "0", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x1]", S "1", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x2]", S "2", UPD)                                                         \
+    NIIDMIX_SEG_SKIPBLK("%[x3]", S "3", UPD)
 #define NIIDMIX_SEG_WALK_X(UPD, MSK, RMSK, RIN)                                                      \
     asm volatile("s_mov_b32 s36, %[sb0]\n"                                                           \
                  ".Lc_next_%=:\n\t"                                                                  \
@@ -1922,11 +1914,6 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  "s_bfe_u32 s46, s41, 0x80014\n\t"                                                   \
                  "s_lshl_b32 s46, s46, 1\n\t"                                                        \
                  "s_mov_b32 s47, 0\n\t"                                                              \
-                 "s_lshr_b32 s57, s42, 2\n\t"                                                        \
-                 "s_bitcmp1_b32 s42, 0\n\t"                                                          \
-                 "s_cselect_b32 s48, %[w1], %[w0]\n\t"                                               \
-                 "s_bitcmp1_b32 s42, 1\n\t"                                                          \
-                 "s_cselect_b32 s50, %[w1], %[w0]\n\t"                                               \
                  "s_cmp_lt_u32 %[nr], 16\n\t"                                                        \
                  "s_cbranch_scc1 .Lseg_small_%=\n\t"                                                 \
                  NIIDMIX_SEG_LOOP("", UPD)                                                           \
@@ -1958,8 +1945,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                    [w0] "s"(w0), [w1] "s"(w1), [l8] "v"(lane8), [nr] "s"(nr), [o1] "i"(RB),            \
                    [o2] "i"(2 * RB), [o3] "i"(3 * RB), [o4] "i"(4 * RB), [o5] "i"(5 * RB) RIN         \
                  : "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", \
-                   "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s57", "m0", "scc",   \
-                   "memory")
+                   "s47", "m0", "scc", "memory")
 // segp: the segment words (int4 per segment); the tile's segments [sb0, sb1) are fetched 64 at a time
 // INSIDE the asm (lane j: segment j's words), so no VALU address arithmetic sits between the tile's
 // init and its walk -- hipcc otherwise moved the pinned tuple out of v[32:63] to make room for it
@@ -1970,7 +1956,7 @@ __device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int
     uint64_t x0, x1, x2, x3, pr;
     uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
     if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
-    else NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_FAST, NIIDMIX_MSK_FAST);
+    else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
     (void)pr;
 }
 typedef float Rem32 __attribute__((ext_vector_type(32)));
@@ -1989,11 +1975,11 @@ __device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp,
     if constexpr (EXACT && NREM == 16)
         NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
     else if constexpr (NREM == 16)
-        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
+        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
     else if constexpr (EXACT)
         NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
     else
-        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
+        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
     (void)pr;
 }
 
