@@ -317,12 +317,8 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
     round-robin (round k of every variant before round k + 1 of any, so that drifts of the host's
     speed hit all of them alike), each timed over `rounds` rounds after one warm-up round:
       cpu_only            the same rounds with the mixing removed (the CPU part of the round);
-      row_streamed        the plugin's default: the parameters stay resident in HBM, each node's
-                          gradient row goes H2D right after its backward(), the device applies the
-                          SGD step and mixes, the mixed rows come back while the next round trains
-                          (deferred write-back; d_sgd._StepEngine);
-      row_streamed_cpu_step  the same with the SGD step on the CPU (NIIDMIX_DEVICE_STEP=0): the
-                          parameter rows go H2D right after each optimizer.step();
+      row_streamed        the plugin's default: rows go H2D right after their optimizer.step(),
+                          the mixed rows come back while the next round trains (deferred write-back);
       row_streamed_sync   the same, but next_step waits for every mixed row before returning;
       windowed            the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0);
       fused_*             the same two with --clique-gradient (gradient mean + SGD step + mixing
@@ -349,12 +345,11 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         def forward(self, x, params):
             return torch.nn.functional.log_softmax(self.fc(x), dim=1)
 
-    variants = ["cpu_only", "row_streamed", "row_streamed_cpu_step", "row_streamed_sync", "windowed"]
+    variants = ["cpu_only", "row_streamed", "row_streamed_sync", "windowed"]
     if cliques:
         variants += ["fused_row_streamed", "fused_windowed"]
     orig, orig_rs = d_sgd.average, d_sgd._row_streamed
     env_res = os.environ.get("NIIDMIX_RESIDENT")
-    env_step = os.environ.get("NIIDMIX_DEVICE_STEP")
 
     def make(v):
         fused = v.startswith("fused")
@@ -364,8 +359,7 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
                   "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": batch,
                                 "initial-averaging": False, "clique-gradient": fused,
                                 "unbiased-gradient": False, "mixing-mode": mode,
-                                "deferred-writeback": v in ("row_streamed", "row_streamed_cpu_step",
-                                                            "fused_row_streamed")}}
+                                "deferred-writeback": v in ("row_streamed", "fused_row_streamed")}}
         torch.manual_seed(3)
         nodes = []
         for r in range(n):
@@ -380,8 +374,6 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             d_sgd._row_streamed = lambda p: False
         if v.endswith("windowed"):
             os.environ["NIIDMIX_RESIDENT"] = "0"          # read when the engine is built
-        if v == "row_streamed_cpu_step":
-            os.environ["NIIDMIX_DEVICE_STEP"] = "0"
         try:
             for key in ("wait_s", "enqueue_s"):
                 d_sgd.round_stats[key] = 0.0
@@ -397,11 +389,10 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
                 st["wait"] += d_sgd.round_stats["wait_s"]
         finally:
             d_sgd.average, d_sgd._row_streamed = orig, orig_rs
-            for key, val in (("NIIDMIX_RESIDENT", env_res), ("NIIDMIX_DEVICE_STEP", env_step)):
-                if val is None:
-                    os.environ.pop(key, None)
-                else:
-                    os.environ[key] = val
+            if env_res is None:
+                os.environ.pop("NIIDMIX_RESIDENT", None)
+            else:
+                os.environ["NIIDMIX_RESIDENT"] = env_res
 
     d_sgd.MAX_ENGINES = max(d_sgd.MAX_ENGINES, len(variants))
     sts = {v: make(v) for v in variants}
@@ -425,7 +416,6 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         res[v] = out
     d_sgd._engines.clear()
     d_sgd._fused_engines.clear()
-    d_sgd._step_engines.clear()
     del sts
     torch.cuda.empty_cache()
     return res

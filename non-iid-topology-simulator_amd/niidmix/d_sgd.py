@@ -403,171 +403,6 @@ class _Engine:
 
 
 
-def _device_step_ok(params):
-    """The plain round's own-gradient SGD step may run on the device (_StepEngine): momentum 0 (the
-    reference's default, d_sgd.py:262-263); NIIDMIX_DEVICE_STEP=0 keeps the step on the CPU."""
-    if os.environ.get("NIIDMIX_DEVICE_STEP", "1") == "0":
-        return False
-    return float(params["algorithm"].get("learning-momentum", 0.0)) == 0.0
-
-
-def _plain_sgd(params, nodes):
-    """Every node's optimizer is the plain torch SGD this plugin's optimizer() builds (momentum,
-    weight decay and dampening 0, the round's learning rate) over exactly its model's parameters:
-    its step is p.add_(g, alpha=-lr), which the device reproduces bit for bit."""
-    lr = float(params["algorithm"]["learning-rate"])
-    for n in nodes:
-        opt = n.get("optimizer")
-        if type(opt) is not torch.optim.SGD or len(opt.param_groups) != 1:
-            return False
-        g = opt.param_groups[0]
-        if (float(g["lr"]) != lr or g["momentum"] != 0 or g["weight_decay"] != 0 or g["nesterov"]
-                or g.get("maximize", False) or g["dampening"] != 0):
-            return False
-        if [id(q) for q in g["params"]] != [id(q) for q in n["model"].parameters()]:
-            return False
-    return True
-
-
-class _StepEngine:
-    """The plain D-SGD round (gradient(), then average(): d_sgd.py:47-52, :217-220) with the
-    own-gradient SGD step on the device.  The parameters stay resident in HBM from one round to the
-    next (round k's mixed output is round k + 1's input, niidmix.slab.ResidentRound keep=0); each
-    node's gradient row goes up right after its backward(); after the last node the device applies
-    p.add_(g, alpha=-lr) (bit for bit torch's SGD step with momentum 0, k_sgd_step_rows) and mixes;
-    the mixed rows come back while the next round trains.  The CPU runs no optimizer step and
-    sends no parameters.  Parameters go up in the first round, and again whenever the host copy
-    no longer matches the resident one: checked every round on a 64-column window of every row
-    (rotating), and init() invalidates (initial averaging rewrites the models on the CPU).
-    .grad keeps the node's own gradient, as after the reference's step."""
-
-    def __init__(self, nodes, topology, params, devices):
-        from .ops import Mixer
-        from .slab import NodeSlab, ResidentRound, fused_op
-        self.topology = topology
-        self.weights_id = id(topology.get("weights"))
-        self.lr = float(params["algorithm"]["learning-rate"])
-        self.slab = NodeSlab([n["model"] for n in nodes])
-        n, p = self.slab.n, self.slab.p
-        csr = to_csr(topology)
-        if csr.n != n:
-            raise ValueError(f"topology has {csr.n} nodes, {n} models given")
-        self.devices = devices
-        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=devices[0])
-        self.gstage = torch.empty((n, p), dtype=torch.float32, pin_memory=True)
-        rows = list(range(n))
-        self.resident = ResidentRound(
-            lambda dev, part: fused_op(dev, part, None, rows, self.lr,
-                                       self.mixer if dev == devices[0] else self.mixer.to(dev)),
-            n, p, devices, block=_row_block(), n_in=2, n_out=1, keep=0)
-        self.on_device = False          # the resident parameters equal the host's
-        self.resends = 0
-        self._col = 0
-
-    @staticmethod
-    def fits(nodes, devices):
-        from .slab import ResidentRound
-        p = sum(q.numel() for q in nodes[0]["model"].parameters())
-        return ResidentRound.fits(len(nodes), p, devices, buffers=3)
-
-    def begin_round(self):
-        self.resident.begin(self.slab.host, self.gstage, outs=(self.slab.host,),
-                            send=(not self.on_device, True))
-
-    def grad_ready(self, i, model):
-        """Node i's backward() is done: its gradient row goes to the pinned staging slab (zeros
-        for a parameter without gradient: p + (-lr) * 0 == p, as SGD skipping it)."""
-        row, off = self.gstage[i], 0
-        for q, (_, k) in zip(model.parameters(), self.slab.shapes):
-            if q.grad is None:
-                row[off:off + k].zero_()
-            else:
-                row[off:off + k].copy_(q.grad.detach().reshape(-1))
-            off += k
-        self.resident.row_ready(i)
-
-    def verify(self):
-        """After the round's training (every mixed row is back): does the host still hold what the
-        device holds?  A 64-column window of every row, bit for bit; otherwise every parameter
-        row goes up with this round's gradients."""
-        if not self.on_device:
-            return True
-        pt = self.resident.parts[0]
-        w = min(64, pt["w"])
-        c0 = self._col % max(1, pt["w"] - w + 1)
-        self._col += 4099
-        host = self.slab.host[:, pt["c0"] + c0:pt["c0"] + c0 + w].contiguous().view(torch.int32)
-        dev = pt["ins"][0][:, c0:c0 + w].view(torch.int32).cpu()
-        if torch.equal(host, dev):
-            return True
-        logging.warning("  models changed outside the mixing round: parameters re-sent")
-        self.resends += 1
-        self.resident.resend(0)
-        return False
-
-    def step_mix(self, mode, defer=False):
-        if self.resident.hosts is None:
-            self.begin_round()
-        self.resident.mix(mode)
-        self.on_device = True
-        if not defer:
-            self.resident.wait_all()
-
-    def wait_row(self, i):
-        self.resident.wait_row(i)
-
-    def wait_all(self):
-        self.resident.wait_all()
-
-    def invalidate(self):
-        self.wait_all()
-        self.on_device = False
-
-    def valid_for(self, nodes, topology, params):
-        return (topology is self.topology and id(topology.get("weights")) == self.weights_id
-                and float(params["algorithm"]["learning-rate"]) == self.lr
-                and self.slab.owns([n["model"] for n in nodes]))
-
-    def owns(self, nodes):
-        return self.slab.owns([n["model"] for n in nodes])
-
-    def set_topology(self, topology):
-        from .ops import Mixer
-        csr = to_csr(topology)
-        if csr.n != self.slab.n:
-            raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
-        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=self.devices[0])
-        for pt in self.resident.parts:
-            pt["mixer"] = self.mixer if pt["dev"] == self.devices[0] else self.mixer.to(pt["dev"])
-        self.topology = topology
-        self.weights_id = id(topology.get("weights"))
-
-
-_step_engines = {}
-
-
-def _step_engine(nodes, topology, params):
-    """The device-step engine of this node list, or None (its buffers do not fit: the CPU steps)."""
-    key = id(nodes)
-    eng = _step_engines.get(key)
-    if eng is not None and not eng.valid_for(nodes, topology, params) and eng.owns(nodes) and \
-            float(params["algorithm"]["learning-rate"]) == eng.lr:
-        eng.set_topology(topology)                   # same nodes, new graph: keep the slab
-    if eng is None or not eng.valid_for(nodes, topology, params):
-        devices = _devices(nodes)
-        if not _resident_ok() or not _plain_sgd(params, nodes) or \
-                not _StepEngine.fits(nodes, devices):
-            return None
-        synchronize()
-        _engines.pop(key, None)                      # one pinned slab per node list
-        eng = _StepEngine(nodes, topology, params, devices)
-        _step_engines.pop(key, None)
-        _step_engines[key] = eng
-        while len(_step_engines) > MAX_ENGINES:
-            _step_engines.pop(next(iter(_step_engines)))
-    return eng
-
-
 _engines = {}
 # engines (pinned slab + device buffers) kept per node list, the most recent ones
 MAX_ENGINES = int(os.environ.get("NIIDMIX_MAX_ENGINES", 4))
@@ -584,7 +419,7 @@ def synchronize():
     """Wait until the mixed parameters of the last round are all back in the nodes' models.
     next_step may return while they stream back (deferred write-back, _deferred_ok); everything in
     this module that reads or writes the models waits first, and so must any other reader."""
-    for eng in list(_engines.values()) + list(_fused_engines.values()) + list(_step_engines.values()):
+    for eng in list(_engines.values()) + list(_fused_engines.values()):
         eng.wait_all()
 
 
@@ -687,8 +522,6 @@ def _loader(node, params):
 def init(nodes, topology, params):
     logging.basicConfig(level=getattr(logging, params["meta"]["log"].upper(), None))
     synchronize()
-    for eng in _step_engines.values():
-        eng.invalidate()                                  # the models may be rewritten below
     state = {"nodes": nodes, "topology": topology, "step": 0}
     for n in nodes:
         n["train-iterator"] = _loader(n, params)
@@ -772,21 +605,16 @@ def next_step(state, params, rundir):
     # plain D-SGD (own gradient, then mixing): the row-streamed round — each node's rows go to the
     # GPU right after its optimizer.step() and come back while the next round trains
     streamed = not sample and not _averages_gradients(params) and _row_streamed(params)
-    # ... and with momentum 0 the SGD step on the device too: only the gradient rows go up
-    seng = (_step_engine(active, topology, params)
-            if streamed and _device_step_ok(params) else None)
-    eng = _engine(active, topology) if streamed and seng is None else None
+    eng = _engine(active, topology) if streamed else None
     # gradient averaging, momentum 0: the fused device round, row-streamed too — each node's
     # parameter and gradient rows go up right after its backward()
     feng = (_fused_engine(active, topology, params)
             if not sample and _fused_ok(params) and _row_streamed(params) else None)
-    if eng is None and feng is None and seng is None:
+    if eng is None and feng is None:
         synchronize()
     if feng is not None:
         feng.begin_round()
-    if seng is not None:
-        seng.begin_round()
-    weng = seng if seng is not None else eng if eng is not None else feng
+    weng = eng if eng is not None else feng
     losses, epoch_done = {}, {}
     clock = time.perf_counter
     for i, node in enumerate(active):                     # local training (CPU)
@@ -804,10 +632,6 @@ def next_step(state, params, rundir):
         if feng is not None:
             t0 = clock()
             feng.row_ready(i)                             # its parameters and gradients are final
-            round_stats["enqueue_s"] += clock() - t0
-        if seng is not None:
-            t0 = clock()
-            seng.grad_ready(i, node["model"])             # its gradient is final
             round_stats["enqueue_s"] += clock() - t0
         rest = _peek(node["train-iterator"])
         done = rest is None
@@ -830,15 +654,6 @@ def next_step(state, params, rundir):
             eng, defer = feng, True
         elif _fused_ok(params):
             fused_round(active, topology, params)         # ★ GPU: gradient + step + mixing
-        elif seng is not None:
-            t0 = clock()
-            seng.verify()
-            logging.info("  own-gradient SGD step + averages of models (GPU, %s, row-streamed)",
-                         _mode(params))
-            seng.step_mix(_mode(params), defer=True)      # ★ GPU: step + mixing
-            round_stats["enqueue_s"] += clock() - t0
-            round_stats["rounds"] += 1
-            eng, defer = seng, True
         elif eng is not None:
             t0 = clock()
             eng.wait_all()                                # (every node trained: nothing pending)

@@ -374,19 +374,14 @@ class ResidentRound:
     MultiDeviceRound (bitwise the one-GPU round).
 
       make_op(dev, part) -> op(ins, outs, mode, kernel)   the device op of one stripe
-                            (part: the stripe's dict; ops may keep state in it)
-    keep=k: input k stays resident from one round to the next -- after each op it trades buffers
-    with output 0, so the next round's op reads this round's (mixed) output as input k, and
-    begin(send=...) need not send it again (the device-step round, niidmix.d_sgd._StepEngine)."""
+                            (part: the stripe's dict; ops may keep state in it)"""
 
-    def __init__(self, make_op, n, p, devices, block=8, align=1024, n_in=1, n_out=1, keep=None):
+    def __init__(self, make_op, n, p, devices, block=8, align=1024, n_in=1, n_out=1):
         from .shard import column_stripe
         self.n, self.p = n, p
         self.block = max(1, int(block))
         self.nblk = -(-n // self.block)
         self.n_in, self.n_out = n_in, n_out
-        self.keep = keep
-        self._send = [True] * n_in
         self.devices = [torch.device(d) for d in devices]
         world = len(self.devices)
         self.parts = []
@@ -424,13 +419,10 @@ class ResidentRound:
     def host(self):
         return None if self.hosts is None else self.hosts[0]
 
-    def begin(self, *hosts, outs=None, send=None):
+    def begin(self, *hosts, outs=None):
         """Start a round: `hosts` are the pinned [N, P] input slabs (n_in of them), `outs` the host
-        slabs the outputs return to (default: the first n_out inputs).  Nothing is sent yet.
-        send[k] False: input k is not sent this round (resident from the last one, keep=k)."""
+        slabs the outputs return to (default: the first n_out inputs).  Nothing is sent yet."""
         assert len(hosts) == self.n_in
-        self._send = [True] * self.n_in if send is None else [bool(v) for v in send]
-        assert len(self._send) == self.n_in
         for h in hosts:
             assert h.shape == (self.n, self.p) and h.dtype == torch.float32 and h.stride(1) == 1
         self.hosts = list(hosts)
@@ -453,25 +445,11 @@ class ResidentRound:
                 s.wait_event(pt["ev_mix"])         # the previous round's op has read the inputs
                 pt["ev_mix"] = None
             w = pt["w"]
-            for k, (h, d) in enumerate(zip(self.hosts, pt["ins"])):
-                if self._send[k]:
-                    _copy2d(d.data_ptr() + r0 * w * 4, w * 4,
-                            h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4,
-                            w * 4, rows, 0, s)
+            for h, d in zip(self.hosts, pt["ins"]):
+                _copy2d(d.data_ptr() + r0 * w * 4, w * 4,
+                        h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4, w * 4,
+                        rows, 0, s)
         self._sent[b] = True
-
-    def resend(self, k):
-        """Input k goes up after all (its resident copy is stale): the blocks already sent get it
-        now, the others with their own H2D."""
-        if self._send[k]:
-            return
-        send = self._send
-        self._send = [j == k for j in range(self.n_in)]
-        for b in range(self.nblk):
-            if self._sent[b]:
-                self._h2d(b)
-        send[k] = True
-        self._send = send
 
     def row_ready(self, i):
         """Row i of the input slabs is final for this round: send its block once it is complete."""
@@ -518,11 +496,6 @@ class ResidentRound:
                     e = torch.cuda.Event()
                     e.record(sd)
                     done[b].append(e)
-                if self.keep is not None:
-                    # this round's output is the next round's resident input; the next op (which
-                    # updates that input in place) waits for this D2H (sm.wait_stream(sd) above)
-                    k = self.keep
-                    pt["ins"][k], pt["outs"][0] = pt["outs"][0], pt["ins"][k]
         self._done = done
         self.hosts = None                           # row_ready() is a no-op until begin()
         self._timing = (timing, t0, t_ev, unsent)
@@ -564,8 +537,7 @@ def mixing_op(dev, part, mixer):
 def fused_op(dev, part, grad_op, step_rows, lr, mixer, grad_writeback=True):
     """ResidentRound device op of the round with gradient averaging (FusedRoundRunner's per-window
     arithmetic on the whole stripe): ins = [params, grads] -> averaged gradients (outs[1]) -> SGD
-    step of the stepped rows on the parameters in place -> mixing into outs[0].  grad_op None: the
-    plain round's own gradients (no averaging; the device-step round)."""
+    step of the stepped rows on the parameters in place -> mixing into outs[0]."""
     from . import ops
     part["mixer"] = mixer
     rows = torch.as_tensor(step_rows, dtype=torch.int32).to(dev)
@@ -573,16 +545,13 @@ def fused_op(dev, part, grad_op, step_rows, lr, mixer, grad_writeback=True):
 
     def op(ins, outs, mode, kernel):
         xp, xg = ins
-        if grad_op is None:                   # the node's own gradient (plain D-SGD)
-            gm = xg
-        elif len(outs) > 1:
+        if len(outs) > 1:
             gm = outs[1]
         else:                                 # no write-back of the averaged gradients
             if "dm" not in part:
                 part["dm"] = torch.empty_like(xg)
             gm = part["dm"]
-        if grad_op is not None:
-            grad_op(xg, out=gm)
+        grad_op(xg, out=gm)
         if rows.numel():
             ops.sgd_step_rows(xp, gm, rows, neg_lr)
         part["mixer"](xp, out=outs[0], mode=mode, kernel=kernel)

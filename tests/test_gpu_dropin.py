@@ -159,113 +159,88 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
         assert torch.equal(u, v)
 
 
-def _ring16_rounds(mix, oracle_mod, rounds=7, sync_each=True, modify_at=None, n=16):
-    """Training rounds of a 16-node ring of linear MNIST-shaped models (run.py reads models at
-    every 3rd step): `mix` "gpu" (the drop-in) or "oracle" (the reference loop does the mixing).
-    Returns the synchronised parameter slab after each round (sync_each) or after the last, and
-    whether a row-streamed engine still had rows in flight when next_step returned.  modify_at=k:
-    after round k the driver rewrites node 5's weights (+0.25), as a user could between rounds."""
-    from niidmix import d_sgd
-    torch.manual_seed(1337)
-    params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
-              "topology": {"name": "ring"},
-              "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 3,
-                         "log-consensus-distance": False},
-              "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 25,
-                            "initial-averaging": False, "clique-gradient": False,
-                            "unbiased-gradient": False, "deferred-writeback": True}}
-
-    class Net(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.fc = torch.nn.Linear(784, 10)
-
-        def forward(self, x, params):
-            return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
-
-    g = torch.Generator().manual_seed(7)
-    data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
-            for _ in range(n * 200)]
-    nodes = []
-    for r in range(n):
-        mdl = Net()
-        nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
-                      "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
-    edges = {r: [(r + 1) % n, (r - 1) % n] if r % 2 else [(r - 1) % n, (r + 1) % n]
-             for r in range(n)}
-    from niidmix.topology import mh_csr
-    topo = {"edges": edges, "weights": torch.from_numpy(mh_csr(n, edges).dense())}
-    orig, orig_rs = d_sgd.average, d_sgd._row_streamed
-    if mix == "oracle":
-        d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
-        d_sgd._row_streamed = lambda p: False
-
-    def slab():
-        return torch.stack([torch.cat([q.detach().reshape(-1) for q in nd["model"].parameters()])
-                            for nd in nodes]).clone()
-    snaps, pend = [], []
-    try:
-        state, _, _ = d_sgd.init(nodes, topo, params)
-        for k in range(rounds):
-            state, losses, done, active = d_sgd.next_step(state, params, None)
-            eng = d_sgd._step_engines.get(id(nodes)) or d_sgd._engines.get(id(nodes))
-            pend.append(bool(eng is not None and eng.resident is not None and
-                             eng.resident.pending))
-            if not sync_each:
-                continue                   # the next round's training waits row by row
-            d_sgd.synchronize()
-            snaps.append(slab())
-            if modify_at == k:
-                with torch.no_grad():
-                    nodes[5]["model"].fc.weight.add_(0.25)
-        if not sync_each:
-            d_sgd.synchronize()
-            snaps.append(slab())
-    finally:
-        d_sgd.average, d_sgd._row_streamed = orig, orig_rs
-    return snaps, pend, nodes
-
-
-@pytest.mark.parametrize("resident,step", [("1", "1"), ("1", "0"), ("0", "1")])
-def test_training_rounds_deferred_writeback(resident, step, gpu, oracle_mod, monkeypatch):
-    """The row-streamed round with deferred write-back, on a 16-node ring of linear MNIST-shaped
-    models over 7 rounds: every round's parameters equal, bit for bit, those of the reference loop
-    doing the mixing (oracle) once synchronised.  step=1 (the default): the SGD step on the device,
-    only the gradient rows go up, the parameters stay resident (d_sgd._StepEngine); step=0: the CPU
-    steps and the parameter rows go up after each optimizer.step().  next_step really returns early
-    on rounds where run.py reads no model, and returns synchronised on the rounds where run.py's
-    should_log (every 3rd step here) reads them; resident=0 runs the windowed engine (always
-    synchronous)."""
+@pytest.mark.parametrize("resident", ["1", "0"])
+def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypatch):
+    """The row-streamed round (rows go H2D right after their optimizer.step(), the mixed rows come
+    back while the next round trains; niidmix.slab.ResidentRound) with deferred write-back, on a
+    16-node ring of linear MNIST-shaped models over 7 rounds: every round's parameters equal, bit for
+    bit, those of the reference loop doing the mixing (oracle) once synchronised.  next_step really
+    returns early on rounds where run.py reads no model, and returns synchronised on the rounds
+    where run.py's should_log (every 3rd step here) reads them; resident=0 runs the windowed
+    engine (always synchronous)."""
     from niidmix import d_sgd
     monkeypatch.setenv("NIIDMIX_RESIDENT", resident)
-    monkeypatch.setenv("NIIDMIX_DEVICE_STEP", step)
     monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")          # ragged last block (16 = 5 x 3 + 1)
-    a, pend, nodes = _ring16_rounds("gpu", oracle_mod)
-    assert (id(nodes) in d_sgd._step_engines) == (resident == "1" and step == "1")
-    b, _, _ = _ring16_rounds("oracle", oracle_mod)
+    n = 16
+
+    def run(mix, sync_each=True):
+        torch.manual_seed(1337)
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
+                  "topology": {"name": "ring"},
+                  "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 3,
+                             "log-consensus-distance": False},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 25,
+                                "initial-averaging": False, "clique-gradient": False,
+                                "unbiased-gradient": False, "deferred-writeback": True}}
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc = torch.nn.Linear(784, 10)
+
+            def forward(self, x, params):
+                return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+        g = torch.Generator().manual_seed(7)
+        data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+                for _ in range(n * 200)]
+        nodes = []
+        for r in range(n):
+            mdl = Net()
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        edges = {r: [(r + 1) % n, (r - 1) % n] if r % 2 else [(r - 1) % n, (r + 1) % n]
+                 for r in range(n)}
+        from niidmix.topology import mh_csr
+        topo = {"edges": edges, "weights": torch.from_numpy(mh_csr(n, edges).dense())}
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False
+        snaps, pend = [], []
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for _ in range(7):
+                state, losses, done, active = d_sgd.next_step(state, params, None)
+                eng = d_sgd._engines.get(id(nodes))
+                pend.append(bool(eng is not None and eng.resident is not None and
+                                 eng.resident.pending))
+                if not sync_each:
+                    continue                   # the next round's training waits row by row
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+            if not sync_each:
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+        return snaps, pend
+
+    a, pend = run("gpu")
+    b, _ = run("oracle")
     for k, (u, v) in enumerate(zip(a, b)):
         assert torch.equal(u, v), k
-    a7, _, _ = _ring16_rounds("gpu", oracle_mod, sync_each=False)
+    a7, _ = run("gpu", sync_each=False)
     assert torch.equal(a7[-1], b[-1])
     if resident == "1":
         # state['step'] after round k is k + 1: run.py reads models at steps 3 and 6
         assert pend == [True, True, False, True, True, False, True]
     else:
         assert not any(pend)
-
-
-def test_device_step_resends_modified_models(gpu, oracle_mod, monkeypatch):
-    """The device-step round keeps the parameters resident between rounds; when the driver rewrites
-    a model between rounds, the round's check (a 64-column window of every row) finds the host copy
-    changed and sends every parameter row again: still bitwise the reference loop with the same
-    rewrite, and exactly one re-send."""
-    from niidmix import d_sgd
-    monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")
-    a, _, nodes = _ring16_rounds("gpu", oracle_mod, rounds=5, modify_at=2)
-    assert d_sgd._step_engines[id(nodes)].resends == 1
-    b, _, _ = _ring16_rounds("oracle", oracle_mod, rounds=5, modify_at=2)
-    for k, (u, v) in enumerate(zip(a, b)):
-        assert torch.equal(u, v), k
 
 
 @pytest.mark.parametrize("alg", ["clique", "unbiased"])

@@ -75,26 +75,3 @@ def test_mixing_devices_policy(monkeypatch):
     assert mixing_devices(3 * MIN_STRIPE_COLS, devs) == devs[:3]
     monkeypatch.setenv("NIIDMIX_DEVICES", "2,5")
     assert mixing_devices(1 << 20) == [torch.device("cuda", 2), torch.device("cuda", 5)]
-
-
-def test_device_step_eligibility(monkeypatch):
-    """The plain round runs its SGD step on the device only for momentum 0 and the plain SGD the
-    plugin's optimizer() builds over each model's own parameters (d_sgd._device_step_ok,
-    _plain_sgd); anything else keeps the step on the CPU."""
-    from niidmix import d_sgd
-    params = {"algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0}}
-    models = [torch.nn.Linear(5, 2) for _ in range(3)]
-    nodes = [{"model": m, "optimizer": d_sgd.optimizer(m, params)} for m in models]
-    assert d_sgd._device_step_ok(params) and d_sgd._plain_sgd(params, nodes)
-    monkeypatch.setenv("NIIDMIX_DEVICE_STEP", "0")
-    assert not d_sgd._device_step_ok(params)
-    monkeypatch.delenv("NIIDMIX_DEVICE_STEP")
-    assert not d_sgd._device_step_ok({"algorithm": {"learning-rate": 0.1, "learning-momentum": 0.9}})
-    other_lr = {"algorithm": {"learning-rate": 0.05, "learning-momentum": 0.0}}
-    assert not d_sgd._plain_sgd(other_lr, nodes)
-    wd = dict(nodes[1], optimizer=torch.optim.SGD(models[1].parameters(), lr=0.1, weight_decay=1e-4))
-    assert not d_sgd._plain_sgd(params, [nodes[0], wd, nodes[2]])
-    adam = dict(nodes[1], optimizer=torch.optim.Adam(models[1].parameters(), lr=0.1))
-    assert not d_sgd._plain_sgd(params, [nodes[0], adam, nodes[2]])
-    swapped = dict(nodes[1], optimizer=d_sgd.optimizer(models[2], params))
-    assert not d_sgd._plain_sgd(params, [nodes[0], swapped, nodes[2]])
