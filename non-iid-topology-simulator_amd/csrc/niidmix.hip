@@ -1773,8 +1773,9 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
 // saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
 #define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
-// the same for tiles whose rows all sit in the first 12 / 8 / 4 slots (a 1000-node d-clique's 9
-// gateway rows form their own tile: 12 adds per position instead of 16)
+// the same for tiles whose rows all sit in the first n slots: a 1000-node d-clique is cut into
+// tiles of 16, 15 x 5 and its 9 gateway rows, a 10 000-node one into 15 x 2 and 14 x 5 rows; a tile
+// adds only its own rows (row counts 9-15 exactly, 8 and 4 rounded up)
 #define NIIDMIX_ADD4(T)                                                                             \
     "v_pk_add_f32 v[32:33], v[32:33], " T "\n\tv_pk_add_f32 v[34:35], v[34:35], " T "\n\t"          \
     "v_pk_add_f32 v[36:37], v[36:37], " T "\n\tv_pk_add_f32 v[38:39], v[38:39], " T "\n\t"
@@ -1798,6 +1799,25 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 #define NIIDMIX_UPD_FAST12(XD)                                                                      \
     NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMA1("v[48:49]", XD) NIIDMIX_FMA1("v[50:51]", XD)                 \
     NIIDMIX_FMA1("v[52:53]", XD) NIIDMIX_FMA1("v[54:55]", XD)
+// one loop per row count 9..15 too (tiles of 14-15 rows: 10 000 nodes; 15: 1000 nodes)
+#define NIIDMIX_ADD9(T) NIIDMIX_ADD8(T) "v_pk_add_f32 v[48:49], v[48:49], " T "\n\t"
+#define NIIDMIX_ADD10(T) NIIDMIX_ADD9(T) "v_pk_add_f32 v[50:51], v[50:51], " T "\n\t"
+#define NIIDMIX_ADD11(T) NIIDMIX_ADD10(T) "v_pk_add_f32 v[52:53], v[52:53], " T "\n\t"
+#define NIIDMIX_ADD13(T) NIIDMIX_ADD12(T) "v_pk_add_f32 v[56:57], v[56:57], " T "\n\t"
+#define NIIDMIX_ADD14(T) NIIDMIX_ADD13(T) "v_pk_add_f32 v[58:59], v[58:59], " T "\n\t"
+#define NIIDMIX_ADD15(T) NIIDMIX_ADD14(T) "v_pk_add_f32 v[60:61], v[60:61], " T "\n\t"
+#define NIIDMIX_SEG_UPD_EXACT9(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD9("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT10(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD10("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT11(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD11("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT13(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD13("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT14(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD14("%[pr]")
+#define NIIDMIX_SEG_UPD_EXACT15(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD15("%[pr]")
+#define NIIDMIX_UPD_FAST9(XD) NIIDMIX_UPD_FAST8(XD) NIIDMIX_FMA1("v[48:49]", XD)
+#define NIIDMIX_UPD_FAST10(XD) NIIDMIX_UPD_FAST9(XD) NIIDMIX_FMA1("v[50:51]", XD)
+#define NIIDMIX_UPD_FAST11(XD) NIIDMIX_UPD_FAST10(XD) NIIDMIX_FMA1("v[52:53]", XD)
+#define NIIDMIX_UPD_FAST13(XD) NIIDMIX_UPD_FAST12(XD) NIIDMIX_FMA1("v[56:57]", XD)
+#define NIIDMIX_UPD_FAST14(XD) NIIDMIX_UPD_FAST13(XD) NIIDMIX_FMA1("v[58:59]", XD)
+#define NIIDMIX_UPD_FAST15(XD) NIIDMIX_UPD_FAST14(XD) NIIDMIX_FMA1("v[60:61]", XD)
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
     "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
@@ -1865,8 +1885,8 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 #define NIIDMIX_REM_IN , [rem] "{v[64:95]}"(rem)
 #define NIIDMIX_REM_IN8 , [rem] "{v[64:79]}"(rem)
 #define NIIDMIX_SEG_WALK(UPD, MSK) NIIDMIX_SEG_WALK_X(UPD, MSK, "", )
-// a run's positions: %[nr] = 16, 12, 8 or 4 rows updated per position (the tile's rows sit in its
-// first nr slots); the 12-, 8- and 4-row loops are copies of the 16-row one with fewer adds
+// a run's positions: %[nr] = 4, 8, 9, ..., 16 rows updated per position (the tile's rows sit in its
+// first nr slots); the smaller loops are copies of the 16-row one with fewer adds
 #define NIIDMIX_SEG_LOOP(S, UPD)                                                                     \
     ".Lseg_loop" S "_%=:\n\t"                                                                       \
     NIIDMIX_SEG_POS("%[x0]", "%[x2]", "o2", S "0", UPD)                                              \
@@ -1922,7 +1942,25 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  "s_cbranch_scc1 .Lseg_loopq_%=\n\t"                                                 \
                  "s_cmp_le_u32 %[nr], 8\n\t"                                                         \
                  "s_cbranch_scc1 .Lseg_looph_%=\n\t"                                                 \
+                 "s_cmp_eq_u32 %[nr], 15\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopn15_%=\n\t"                                               \
+                 "s_cmp_eq_u32 %[nr], 14\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopn14_%=\n\t"                                               \
+                 "s_cmp_eq_u32 %[nr], 13\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopn13_%=\n\t"                                               \
+                 "s_cmp_eq_u32 %[nr], 12\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopt_%=\n\t"                                                 \
+                 "s_cmp_eq_u32 %[nr], 11\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopn11_%=\n\t"                                               \
+                 "s_cmp_eq_u32 %[nr], 10\n\t"                                                        \
+                 "s_cbranch_scc1 .Lseg_loopn10_%=\n\t"                                               \
+                 NIIDMIX_SEG_LOOP("n9", UPD##9)                                                      \
+                 NIIDMIX_SEG_LOOP("n10", UPD##10)                                                    \
+                 NIIDMIX_SEG_LOOP("n11", UPD##11)                                                    \
                  NIIDMIX_SEG_LOOP("t", UPD##12)                                                      \
+                 NIIDMIX_SEG_LOOP("n13", UPD##13)                                                    \
+                 NIIDMIX_SEG_LOOP("n14", UPD##14)                                                    \
+                 NIIDMIX_SEG_LOOP("n15", UPD##15)                                                    \
                  NIIDMIX_SEG_LOOP("h", UPD##8)                                                       \
                  NIIDMIX_SEG_LOOP("q", UPD##4)                                                       \
                  "\n.Lw_masked_%=:\n\t"                                                              \
@@ -2518,11 +2556,12 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
             {                                                            // segment loop (tile.py)
                 const int sb0 = seg_ptr[sub], sb1 = seg_ptr[sub + 1];
                 const int w0 = __float_as_int(seg_w[2 * sub]), w1 = __float_as_int(seg_w[2 * sub + 1]);
-                // rows updated per run position: the tile's used slots rounded up to 4 / 8 / 12 / 16
-                // (wave-uniform; the slots above are unused and never stored)
+                // rows updated per run position: the tile's used slots (9-16 exactly, else rounded up
+                // to 4 / 8; wave-uniform; the slots above are unused and never stored)
                 const uint64_t used = __ballot(lane < RT && d_row >= 0);
                 const int hi = used ? 64 - __builtin_clzll(used) : 1;
-                const int nr = __builtin_amdgcn_readfirstlane(small_loops ? (hi + 3) & ~3 : 16);
+                const int nr = __builtin_amdgcn_readfirstlane(
+                    !small_loops ? 16 : hi <= 4 ? 4 : hi <= 8 ? 8 : hi);
                 // segment words (int4 each): a run: first slot | length << 12 | first skipped row << 20,
                 // weight-select bits, skip bits; a MASKED position: slot | 1 << 30, the rows that take
                 // it, its weight (fp32 bits).  One walker for every tile: walkers specialised by the
