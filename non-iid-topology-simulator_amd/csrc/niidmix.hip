@@ -1771,7 +1771,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // Fixed scratch SGPRs: s38 run length, s39 LDS address, s40 segment index, s41 dx, s42 dy (masked:
 // the remaining rows), s43 dz, s44 weight, s46 skipped row * 2 / row index, s47 position.  VGPR
 // scratch are compiler-allocated operands: x0..x3 rotating row pairs, pr the product, sv0 / sv1 the
-// saved skipped row, q0 / q1 a masked position's product (exact) or row (fast), va the address.
+// saved skipped row (one v_mov_b64 each way), q0 / q1 a masked position's product (exact) or row (fast), va the address.
 #define NIIDMIX_SEG_UPD_EXACT(XD) "v_pk_mul_f32 %[pr], " XD ", s[44:45] op_sel_hi:[1,0]\n\t" NIIDMIX_ADD16("%[pr]")
 // the same for tiles whose rows all sit in the first n slots: a 1000-node d-clique is cut into
 // tiles of 16, 15 x 5 and its 9 gateway rows, a 10 000-node one into 15 x 2 and 14 x 5 rows; a tile
@@ -1832,12 +1832,10 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 #define NIIDMIX_SEG_SKIPBLK(XD, K, UPD)                                                              \
     "\n.Lseg_skip" K "_%=:\n\t"                                                                     \
     "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
-    "v_mov_b32 %[sv0], v32\n\t"                                                                      \
-    "v_mov_b32 %[sv1], v33\n\t"                                                                      \
+    "v_mov_b64 %[sv], v[32:33]\n\t"                                                                 \
     "s_set_gpr_idx_off\n\t" UPD(XD)                                                                  \
     "s_set_gpr_idx_on s46, gpr_idx(DST)\n\t"                                                        \
-    "v_mov_b32 v32, %[sv0]\n\t"                                                                      \
-    "v_mov_b32 v33, %[sv1]\n\t"                                                                      \
+    "v_mov_b64 v[32:33], %[sv]\n\t"                                                                 \
     "s_set_gpr_idx_off\n\t"                                                                          \
     "s_add_u32 s46, s46, 2\n\t"                                                                      \
     "s_branch .Lseg_back" K "_%=\n\t"
@@ -1976,7 +1974,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
                  ".Lw_end_%=:\n\t"                                                                   \
                  "s_waitcnt lgkmcnt(0)"                                                              \
                  : "+{v[32:63]}"(acc), [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2),             \
-                   [x3] "=&v"(x3), [pr] "=&v"(pr), [sv0] "=&v"(sv0), [sv1] "=&v"(sv1),              \
+                   [x3] "=&v"(x3), [pr] "=&v"(pr), [sv] "=&v"(sv),                                   \
                    [q0] "=&v"(q0), [q1] "=&v"(q1), [va] "=&v"(va), [dx] "=&v"(dx), [dy] "=&v"(dy),  \
                    [dz] "=&v"(dz), [vo] "=&v"(vo)                                                   \
                  : [sp] "s"(segp), [sb0] "s"(sb0), [sb1] "s"(sb1), [ln] "v"(lane), [base] "s"(base), \
@@ -1992,7 +1990,8 @@ __device__ __forceinline__ void tlds16_walk(Acc16 &acc, const int32_t *segp, int
                                             int w0, int w1, int lane8, int lane, int nr) {
     static_assert(5 * RB < 65536, "ds_read immediate offset");
     uint64_t x0, x1, x2, x3, pr;
-    uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
+    uint64_t sv;
+    uint32_t q0, q1, va, dx, dy, dz, vo;
     if constexpr (EXACT) NIIDMIX_SEG_WALK(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT);
     else NIIDMIX_SEG_WALK(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST);
     (void)pr;
@@ -2009,7 +2008,8 @@ __device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp,
     static_assert(5 * RB < 65536, "ds_read immediate offset");
     static_assert(NREM == 8 || NREM == 16, "8 or 16 register rows");
     uint64_t x0, x1, x2, x3, pr;
-    uint32_t sv0, sv1, q0, q1, va, dx, dy, dz, vo;
+    uint64_t sv;
+    uint32_t q0, q1, va, dx, dy, dz, vo;
     if constexpr (EXACT && NREM == 16)
         NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
     else if constexpr (NREM == 16)
