@@ -1,0 +1,32 @@
+#!/bin/bash
+# round 4 session G: exact default (8 register rows per tile) -- unused register rows not loaded
+# (A/B against the previous build), phase split, SQ counters, bench lines
+out=gpurun_out/r4g
+mkdir -p $out
+export TMPDIR=/tmp
+true > $out/pytest.log
+rc=0
+[ $rc -eq 0 ] || { grep -E "FAILED|Error" $out/pytest.log | head; echo "pytest rc=$rc: stop"; exit 1; }
+for lib in cur prev cur; do
+  L=$PWD/non-iid-topology-simulator_amd/niidmix/libniidmix.so; [ $lib = prev ] && L=$PWD/tools/build/libniidmix_prev.so
+  NIIDMIX_LIB=$L timeout -k 10 300 python -u tools/exact_probe.py --rts 16 --metas seg,rem8,rem16 --reps 2 > $out/exact_probe_$lib.txt 2>&1 || { tail -5 $out/exact_probe_$lib.txt; exit 2; }
+  echo "lib $lib"; grep SUMMARY $out/exact_probe_$lib.txt
+done
+for s in 1 2; do
+  NIIDMIX_LIB=tools/build/libniidmix_split$s.so timeout -k 10 300 python -u tools/exact_probe.py --rts 16 --metas seg,rem8 --reps 2 --no-check > $out/exact_probe_split$s.txt 2>&1 || { tail -5 $out/exact_probe_split$s.txt; exit 3; }
+  echo "split $s"; grep SUMMARY $out/exact_probe_split$s.txt
+done
+P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+P2="SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE"
+i=1
+for c in "$P1" "$P2"; do
+  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $PWD/$out/sq_exact_p$i -o p -- python3 bench.py --no-cpu-baseline --kernel tile-lds-exact --steps 2 --warmup 1 > $out/sq_exact_p$i.log 2>&1 || { echo "sq pass $i failed"; tail -3 $out/sq_exact_p$i.log; exit 4; }
+  i=$((i+1))
+done
+python tools/sq_summary.py k_mix_tile_lds $out/sq_exact_p1 $out/sq_exact_p2 > $out/sq_exact_summary.txt; cat $out/sq_exact_summary.txt
+timeout -k 10 300 python bench.py --kernel tile-lds-exact --steps 20 --no-cpu-baseline > $out/bench_exact_headline.json 2> $out/bench_exact_headline.err || exit 5
+python -c "import json;d=json.load(open('$out/bench_exact_headline.json'));print('headline exact', d['ms_per_step'], 'ms', d['roofline']['frac'])"
+timeout -k 10 600 python bench.py --config dcliques10000 --kernel tile-lds-exact --steps 5 --warmup 2 --no-cpu-baseline > $out/bench_exact10k.json 2> $out/bench_exact10k.err || exit 6
+python -c "import json;d=json.load(open('$out/bench_exact10k.json'));print('10k exact', d['ms_per_step'], 'ms', d['roofline']['frac'])"
+timeout -k 10 300 python bench.py --config ring100 --steps 200 --no-cpu-baseline > $out/bench_ring_cold.json 2> $out/bench_ring_cold.err || exit 7
+python -c "import json;d=json.load(open('$out/bench_ring_cold.json'));print('ring', d['ms_per_step'], d['config'].get('cold_cache_round'))"
