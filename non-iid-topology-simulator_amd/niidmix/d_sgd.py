@@ -602,10 +602,8 @@ def next_step(state, params, rundir):
     sample = params["topology"]["name"] == "sample"
     active = get_sample(state, params, state["step"]) if sample else state["nodes"]
     topology = state["topology"]
-    # plain D-SGD (own gradient, then mixing): the row-streamed round — each node steps right after
-    # its backward() (gradient(), d_sgd.py:51-52, steps every node after all of them trained; a
-    # node's step reads and writes only its own model, so the order changes no bit) and its rows go
-    # to the GPU at once, while the CPU trains the next nodes; they come back during the next round
+    # plain D-SGD (own gradient, then mixing): the row-streamed round — each node's rows go to the
+    # GPU right after its optimizer.step() and come back while the next round trains
     streamed = not sample and not _averages_gradients(params) and _row_streamed(params)
     eng = _engine(active, topology) if streamed else None
     # gradient averaging, momentum 0: the fused device round, row-streamed too — each node's
@@ -616,8 +614,6 @@ def next_step(state, params, rundir):
         synchronize()
     if feng is not None:
         feng.begin_round()
-    if eng is not None:
-        eng.begin_round()
     weng = eng if eng is not None else feng
     losses, epoch_done = {}, {}
     clock = time.perf_counter
@@ -636,11 +632,6 @@ def next_step(state, params, rundir):
         if feng is not None:
             t0 = clock()
             feng.row_ready(i)                             # its parameters and gradients are final
-            round_stats["enqueue_s"] += clock() - t0
-        if eng is not None:
-            node["optimizer"].step()                      # d_sgd.py:51-52, this node's step
-            t0 = clock()
-            eng.row_ready(i)                              # its parameters are final
             round_stats["enqueue_s"] += clock() - t0
         rest = _peek(node["train-iterator"])
         done = rest is None
@@ -664,8 +655,17 @@ def next_step(state, params, rundir):
         elif _fused_ok(params):
             fused_round(active, topology, params)         # ★ GPU: gradient + step + mixing
         elif eng is not None:
-            logging.info("  own gradient applied node by node; computing averages of models "
-                         "(GPU, %s, row-streamed)", _mode(params))
+            t0 = clock()
+            eng.wait_all()                                # (every node trained: nothing pending)
+            eng.begin_round()
+            round_stats["wait_s"] += clock() - t0
+            logging.info("  applying own gradient")
+            for i, n in enumerate(active):                # d_sgd.py:51-52, rows sent as they
+                n["optimizer"].step()                     # become final
+                t0 = clock()
+                eng.row_ready(i)
+                round_stats["enqueue_s"] += clock() - t0
+            logging.info("  computing averages of models (GPU, %s, row-streamed)", _mode(params))
             t0 = clock()
             eng.mix(_mode(params), False, defer=True)     # ★ GPU
             round_stats["enqueue_s"] += clock() - t0
