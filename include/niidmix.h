@@ -23,7 +23,8 @@
  * the full extents of both (NIIDMIX_EALIAS), each slab with its own strides.
  *
  * ABI 4 (this header): niidmix_mix_band_f32 added (banded low-degree graphs, e.g. a ring in its
- * cycle order).
+ * cycle order), niidmix_mix_strip_f32 (column strips for few nodes), register rows in the LDS
+ * tile plan.
  * ABI 3: n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
  * niidmix_grad_segment_mean_f32 and niidmix_grad_segment_mean_blocked_f32 (full extent checks);
  * niidmix_update_rows_f32 added (the 'sample' topology's broadcast); niidmix_mix_ell_f32 added
@@ -129,6 +130,17 @@ int niidmix_mix_ell_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
 int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
                          int64_t p, int k, int band, const int32_t *ell_col, const float *ell_val,
                          const int32_t *ell_len, int mode, void *stream);
+
+/* The same round for FEW nodes (n_rows <= 256; ring 100, BASELINE configs[1]) by column strips:
+ * one wave owns 64 columns of every row, stages them in LDS (n_rows x 256 B) and combines each
+ * output row from there in its ELL order, so each element of x is read from memory once and a
+ * round is one generation of ceil(p / 64) waves.  Any row order.  Descriptors: the ELL arrays of
+ * niidmix_mix_ell_f32 (k = 3, 5 or 8).  x 4-B aligned; x and y: [n_rows, ld].  mode as
+ * niidmix_mix_ell_f32; bit-identical to it (and to niidmix_mix_csr_f32) in EXACT mode.  Round 4
+ * (ABI 4). */
+int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                          int64_t p, int k, const int32_t *ell_col, const float *ell_val,
+                          const int32_t *ell_len, int mode, void *stream);
 
 /* Clique-factored mixing (fast mode only).  For each member m of clique c:
  *   y_m = a_m * x_m + sum_{g < n_groups} c_{m,g} * S_{c,g} + sum_r res_val[r] * x[res_col[r]]

@@ -360,6 +360,48 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 }
 
 // ----------------------------------------------------------------------------------------------
+// Column strips for few nodes (n_rows <= 256; ring 100, BASELINE configs[1]): one wave owns 64
+// columns of EVERY row.  The strip lands in LDS (LDS-DMA, 4 B per lane per row, every row's load in
+// flight at once, no descriptor in front of any load), then each output row is combined from LDS in
+// its ELL order and stored.  Each element of x is read from memory exactly once (the ELL / band
+// kernels read a row up to K times through L2), and a round is one generation of n_strips waves.
+// Same arithmetic, in the same order, as k_mix_ell (z from the row's first entry, self).
+template <bool EXACT, int K>
+__global__ __launch_bounds__(64) void k_mix_strip(const float *__restrict__ x, int64_t ld_x,
+                                                  float *__restrict__ y, int64_t ld_y, int n_rows,
+                                                  int64_t p, const int32_t *__restrict__ ell_col,
+                                                  const float *__restrict__ ell_val,
+                                                  const int32_t *__restrict__ ell_len, int avg_only) {
+    extern __shared__ float strip[];          // [n_rows][64]
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) void glb_void;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t c0 = (int64_t)blockIdx.x * kWave;
+    const int64_t col = c0 + lane;
+    const bool ok = col < p;
+    const float *xs = x + (ok ? col : c0);    // lanes past p read a valid column, store nothing
+    for (int r = 0; r < n_rows; ++r)
+        __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
+                                         (lds_void *)(strip + r * kWave), 4, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // the strip has landed
+    float *dst = y + col;
+#pragma unroll 2
+    for (int r = 0; r < n_rows; ++r) {
+        const int64_t e0 = (int64_t)r * K;
+        const int len = ell_len[r];
+        float xv[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xv[j] = strip[ell_col[e0 + (j < len ? j : 0)] * kWave + lane];
+        const float z = xv[0] * 0.f;          // self * 0 (d_sgd.py:105: self is entry 0)
+        float acc = z;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (j < len) acc = axpy<EXACT>(ell_val[e0 + j], xv[j], acc);      // wave-uniform
+        if (ok) __builtin_nontemporal_store(avg_only ? acc : z + acc, dst + (int64_t)r * ld_y);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Banded low-degree graphs (a ring in its cycle order: every entry of row r is a row r + d, |d| <=
 // B, taken cyclically).  The ELL kernel above is a chain per wave — descriptor load, then the
 // gathers it names, then the store — and reads every row K times.  Here a wave owns R consecutive
@@ -3573,6 +3615,35 @@ int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
 #undef NIIDMIX_BAND_R
 #undef NIIDMIX_BAND
     return check_launch("k_mix_band");
+}
+
+int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,
+                          int64_t p, int k, const int32_t *ell_col, const float *ell_val,
+                          const int32_t *ell_len, int mode, void *stream) {
+    if (n_rows < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    const int avg_only = (mode & NIIDMIX_FLAG_AVERAGE_ONLY) ? 1 : 0;
+    mode &= ~(NIIDMIX_FLAG_AVERAGE_ONLY | NIIDMIX_FLAG_LOW_DEGREE);
+    if (mode != NIIDMIX_MODE_EXACT && mode != NIIDMIX_MODE_FAST)
+        return set_error(NIIDMIX_EINVAL, "unknown mode %d", mode);
+    if (k != 3 && k != 5 && k != 8) return set_error(NIIDMIX_EUNSUPPORTED, "ELL width %d (3, 5 or 8)", k);
+    if (n_rows == 0 || p == 0) return NIIDMIX_OK;
+    if (n_rows > 256) return set_error(NIIDMIX_EUNSUPPORTED, "strip kernel: %lld rows (<= 256)", (long long)n_rows);
+    if (!x || !y || !ell_col || !ell_val || !ell_len) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (overlaps(x, (n_rows - 1) * ld_x + p, y, (n_rows - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    if (reinterpret_cast<uintptr_t>(x) & 3) return set_error(NIIDMIX_EUNSUPPORTED, "x not 4-B aligned");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n_strips = (p + kWave - 1) / kWave;
+    if (n_strips > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many strips");
+    const size_t lds = (size_t)n_rows * kWave * sizeof(float);        // <= 64 KB
+    const dim3 grid((unsigned)n_strips), block(kWave);
+#define NIIDMIX_STRIP(E, KK) hipLaunchKernelGGL((k_mix_strip<E, KK>), grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only)
+#define NIIDMIX_STRIP_K(E) do { if (k == 3) NIIDMIX_STRIP(E, 3); else if (k == 5) NIIDMIX_STRIP(E, 5); else NIIDMIX_STRIP(E, 8); } while (0)
+    if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_STRIP_K(true); else NIIDMIX_STRIP_K(false);
+#undef NIIDMIX_STRIP_K
+#undef NIIDMIX_STRIP
+    return check_launch("k_mix_strip");
 }
 
 int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

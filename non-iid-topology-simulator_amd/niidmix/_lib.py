@@ -64,6 +64,8 @@ SIGNATURES = {
                                            _vp, ctypes.c_int, _vp]),
     "niidmix_mix_band_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int,
                                             ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "niidmix_mix_strip_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, ctypes.c_int, _vp,
+                                             _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_mix_clique_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64,
                                               ctypes.POINTER(CliquePlanC), _vp]),
     "niidmix_mix_clique_blocked_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64,

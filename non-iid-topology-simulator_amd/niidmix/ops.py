@@ -178,6 +178,29 @@ def mix_band(x: torch.Tensor, ell_col: torch.Tensor, ell_val: torch.Tensor, ell_
     _lib.check(rc, "niidmix::mix_band")
 
 
+@torch.library.custom_op("niidmix::mix_strip", mutates_args=("out",))
+def mix_strip(x: torch.Tensor, ell_col: torch.Tensor, ell_val: torch.Tensor, ell_len: torch.Tensor,
+              out: torch.Tensor, k: int, mode: int) -> None:
+    """mix_ell for few nodes (<= STRIP_MAX_ROWS) by column strips staged in LDS (include/niidmix.h
+    niidmix_mix_strip_f32): each element of x is read once; any row order."""
+    _slab("x", x)
+    _slab("out", out, cols=x.shape[1])
+    _req(out.device == x.device, "x and out must be on the same device")
+    n = out.shape[0]
+    _req(n <= STRIP_MAX_ROWS, f"strip kernel: {n} rows (<= {STRIP_MAX_ROWS})")
+    _req(x.shape[0] >= n, f"x has {x.shape[0]} rows, fewer than the {n} output rows")
+    _vec("ell_col", ell_col, torch.int32, x.device, n * k)
+    _vec("ell_val", ell_val, torch.float32, x.device, n * k)
+    _vec("ell_len", ell_len, torch.int32, x.device, n)
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_strip_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n,
+                                        x.shape[1], int(k), ell_col.data_ptr(), ell_val.data_ptr(),
+                                        ell_len.data_ptr(), int(mode), _stream(x))
+    _lib.check(rc, "niidmix::mix_strip")
+
+
+STRIP_MAX_ROWS = 256
+
 # (ELL width, band) pairs the band kernel is built for
 BAND_OF_K = {3: 1, 5: 2}
 
@@ -827,6 +850,10 @@ class Mixer:
             _req(self.ell is not None, "no ELL layout: a row has more than 8 entries")
             mix_ell(x, self.e_col, self.e_val, self.e_len, out, self.ell,
                     EXACT if k == "ell-exact" else FAST)
+        elif k in ("strip-exact", "strip-fast"):
+            _req(self.ell is not None, "no ELL layout: a row has more than 8 entries")
+            mix_strip(x, self.e_col, self.e_val, self.e_len, out, self.ell,
+                      EXACT if k == "strip-exact" else FAST)
         elif k in ("band-exact", "band-fast"):
             _req(self.band is not None, "no band layout: rows are not banded as stored "
                  "(Mixer.device_layout / band_layout gives a ring's cycle order)")

@@ -141,3 +141,68 @@ def test_ring100_band_hipgraph(mode, gpu, oracle_mod):
                 bound = oracle_mod.condition_bound(xin, c.row_ptr, c.col, c.val)
                 ok, worst = oracle_mod.check_tolerance(yout, ref, bound, rtol=RTOL)
                 assert ok, worst
+
+
+@pytest.mark.parametrize("name", ["ring100_p257", "nonfinite_ring8_p16", "n2_ring_linear7850"])
+def test_strip_vs_reference_golden(name, gpu, oracle_mod):
+    """k_mix_strip (column strips staged in LDS, few nodes): the reference's own round, bitwise in
+    exact mode (odd P too: a strip is 64 columns of every row, lanes past P store nothing), within
+    the tolerance in fast mode; rank order (the strip kernel reads any row order)."""
+    from niidmix import ops
+    from niidmix.topology import MixCSR
+    g = load_golden(name)
+    csr = MixCSR(g["row_ptr"], g["col"], g["val"]).validate()
+    m = ops.Mixer(csr=csr, device=gpu)
+    if m.ell is None:
+        pytest.skip("a row has more than 8 entries")
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="strip-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(y, g["y"])
+    yf = m(x, kernel="strip-fast").cpu().numpy()
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(yf, g["y"], bound, rtol=RTOL)
+    assert ok, worst
+
+
+@pytest.mark.parametrize("n,k,p", [(3, 3, 64), (17, 3, 1000), (100, 3, 62006), (256, 3, 130),
+                                   (64, 5, 333), (200, 8, 129)])
+def test_strip_sizes_vs_ell(n, k, p, gpu, oracle_mod):
+    """Strip kernel bitwise the C oracle (exact) on rings and random low-degree graphs of 3-256
+    nodes, ELL widths 3 / 5 / 8, P not a multiple of 64, a strided window of a wider slab, the
+    average-only flag; and the explicit limit (257 rows) is refused."""
+    from niidmix import ops
+    from niidmix.topology import mh_csr
+    rng = np.random.default_rng(n * 7 + k)
+    if k == 3:
+        edges = {i: [(i + 1) % n, (i - 1) % n] if n > 2 else [(i + 1) % n] for i in range(n)}
+    else:
+        edges = {}
+        for i in range(n):
+            nb = rng.choice([j for j in range(n) if j != i], size=k - 1, replace=False)
+            edges[i] = [int(j) for j in nb]
+        for i in list(edges):                     # symmetric graph, at most k - 1 neighbours kept
+            for j in edges[i]:
+                if i not in edges[j]:
+                    edges[j].append(i)
+        edges = {i: v[:k - 1] for i, v in edges.items()}
+        for i in edges:                           # re-symmetrise after the cut
+            edges[i] = [j for j in edges[i] if i in edges[j]]
+    csr = mh_csr(n, edges)
+    m = ops.Mixer(csr=csr, device=gpu)
+    assert m.ell is not None and m.ell <= 8
+    wide = torch.from_numpy(rng.standard_normal((n, p + 6)).astype(np.float32)).to(gpu)
+    x = wide[:, 3:3 + p]                          # ld = p + 6
+    y = m(x, kernel="strip-exact").cpu().numpy()
+    ref = oracle_mod.mix_exact_c(wide.cpu().numpy(), csr.row_ptr, csr.col, csr.val, cols=(3, 3 + p))
+    assert oracle_mod.bitwise_equal(y, ref[:, 3:3 + p])
+    out = torch.empty((n, p), device=gpu)
+    ops.mix_strip(x.contiguous(), m.e_col, m.e_val, m.e_len, out, m.ell, ops.EXACT | ops.AVERAGE_ONLY)
+    ref_avg = torch.empty_like(out)
+    ops.mix_ell(x.contiguous(), m.e_col, m.e_val, m.e_len, ref_avg, m.ell, ops.EXACT | ops.AVERAGE_ONLY)
+    assert torch.equal(out, ref_avg)
+    if n == 256:
+        with pytest.raises(RuntimeError, match="strip kernel"):
+            big = torch.zeros((257, 64), device=gpu)
+            ops.mix_strip(big, torch.zeros(257 * 3, dtype=torch.int32, device=gpu),
+                          torch.zeros(257 * 3, device=gpu), torch.ones(257, dtype=torch.int32, device=gpu),
+                          torch.empty_like(big), 3, ops.EXACT)

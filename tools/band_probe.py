@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """ring100 (P = 62 006) round time per band-kernel shape (rows x column chunks per wave), the ELL
-kernel and the stream copy of the same slab, each as bench.py times it: K rounds in ONE hipGraph,
+kernel, the column-strip kernel and the stream copy of the same slab, each as bench.py times it: K rounds in ONE hipGraph,
 replayed (tuning tool).
 
     python tools/band_probe.py [--rc 1,1:1,2:2,2:4,4] [--steps 20] [--reps 5]
@@ -67,6 +67,15 @@ def main():
         us = graph_round_us(lambda x, y: m(x, out=y, kernel="ell-fast"), xa, xb, a.steps, a.reps)
         print(f"ell CH={ch}         {us[0]:7.2f} / {us[1]:7.2f} us per round (rank order)")
     os.environ.pop("NIIDMIX_ELL_CH", None)
+    for mode, kname in (("fast", "strip-fast"), ("exact", "strip-exact")):
+        us = graph_round_us(lambda x, y: mr(x, out=y, kernel=kname), xa, xb, a.steps, a.reps)
+        print(f"strip {mode:5s}       {us[0]:7.2f} / {us[1]:7.2f} us per round (column strips in LDS)")
+    # the strip kernel's result against the band kernel's (exact: bitwise)
+    ya, yb = torch.empty_like(xa), torch.empty_like(xa)
+    mr(xa, out=ya, kernel="band-exact")
+    mr(xa, out=yb, kernel="strip-exact")
+    torch.cuda.synchronize()
+    print("strip-exact == band-exact:", bool(torch.equal(ya, yb)))
     numel = n * p - (n * p) % 4
     fa, fb = xa.view(-1)[:numel], xb.view(-1)[:numel]
 
