@@ -360,43 +360,62 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 }
 
 // ----------------------------------------------------------------------------------------------
-// Column strips for few nodes (n_rows <= 256; ring 100, BASELINE configs[1]): one wave owns 64
-// columns of EVERY row.  The strip lands in LDS (LDS-DMA, 4 B per lane per row, every row's load in
-// flight at once, no descriptor in front of any load), then each output row is combined from LDS in
-// its ELL order and stored.  Each element of x is read from memory exactly once (the ELL / band
-// kernels read a row up to K times through L2), and a round is one generation of n_strips waves.
-// Same arithmetic, in the same order, as k_mix_ell (z from the row's first entry, self).
-template <bool EXACT, int K>
-__global__ __launch_bounds__(64) void k_mix_strip(const float *__restrict__ x, int64_t ld_x,
-                                                  float *__restrict__ y, int64_t ld_y, int n_rows,
-                                                  int64_t p, const int32_t *__restrict__ ell_col,
-                                                  const float *__restrict__ ell_val,
-                                                  const int32_t *__restrict__ ell_len, int avg_only) {
+// Column strips for few nodes (n_rows <= 256; ring 100, BASELINE configs[1]): a block of SW waves
+// owns 64 columns of EVERY row.  The strip lands in LDS (LDS-DMA, 4 B per lane per row; wave w
+// stages rows w, w + SW, ...; every load in flight at once, no descriptor in front of any of them),
+// then wave w combines the same rows' outputs from LDS in their ELL order and stores them.  Each
+// element of x is read from memory exactly once (the ELL / band kernels read a row up to K times
+// through L2).  The descriptors of a wave's rows are loaded lane-parallel with the strip (lane i:
+// row w + SW i) and handed out by v_readlane: no scalar-load round trip per row.  Same arithmetic,
+// in the same order, as k_mix_ell (z from the row's first entry, self).
+template <bool EXACT, int K, int SW>
+__global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__ x, int64_t ld_x,
+                                                       float *__restrict__ y, int64_t ld_y,
+                                                       int n_rows, int64_t p,
+                                                       const int32_t *__restrict__ ell_col,
+                                                       const float *__restrict__ ell_val,
+                                                       const int32_t *__restrict__ ell_len,
+                                                       int avg_only) {
     extern __shared__ float strip[];          // [n_rows][64]
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) void glb_void;
     const int lane = threadIdx.x & (kWave - 1);
+    const int wave = wave_id();
     const int64_t c0 = (int64_t)blockIdx.x * kWave;
     const int64_t col = c0 + lane;
     const bool ok = col < p;
     const float *xs = x + (ok ? col : c0);    // lanes past p read a valid column, store nothing
-    for (int r = 0; r < n_rows; ++r)
+    for (int r = wave; r < n_rows; r += SW)
         __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
                                          (lds_void *)(strip + r * kWave), 4, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // the strip has landed
+    const int mr = wave + SW * lane;          // the row this lane describes (n_rows <= 64 SW)
+    const bool in = mr < n_rows;
+    const int dlen = in ? ell_len[mr] : 0;
+    int dcol[K];
+    float dval[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        dcol[j] = in ? ell_col[(int64_t)mr * K + j] : 0;
+        dval[j] = in ? ell_val[(int64_t)mr * K + j] : 0.f;
+    }
+    __syncthreads();                          // the whole strip has landed (vmcnt(0) + barrier)
     float *dst = y + col;
-#pragma unroll 2
-    for (int r = 0; r < n_rows; ++r) {
-        const int64_t e0 = (int64_t)r * K;
-        const int len = ell_len[r];
+    const int nw = (n_rows - wave + SW - 1) / SW;                  // rows of this wave
+#pragma unroll 4
+    for (int i = 0; i < nw; ++i) {
+        const int r = wave + SW * i;
+        const int len = __builtin_amdgcn_readlane(dlen, i);
         float xv[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) xv[j] = strip[ell_col[e0 + (j < len ? j : 0)] * kWave + lane];
+        for (int j = 0; j < K; ++j)
+            xv[j] = strip[__builtin_amdgcn_readlane(dcol[j < len ? j : 0], i) * kWave + lane];
         const float z = xv[0] * 0.f;          // self * 0 (d_sgd.py:105: self is entry 0)
         float acc = z;
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            if (j < len) acc = axpy<EXACT>(ell_val[e0 + j], xv[j], acc);      // wave-uniform
+            if (j < len)                                                   // wave-uniform
+                acc = axpy<EXACT>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dval[j]), i)),
+                                  xv[j], acc);
         if (ok) __builtin_nontemporal_store(avg_only ? acc : z + acc, dst + (int64_t)r * ld_y);
     }
 }
@@ -3637,8 +3656,8 @@ int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     const int64_t n_strips = (p + kWave - 1) / kWave;
     if (n_strips > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many strips");
     const size_t lds = (size_t)n_rows * kWave * sizeof(float);        // <= 64 KB
-    const dim3 grid((unsigned)n_strips), block(kWave);
-#define NIIDMIX_STRIP(E, KK) hipLaunchKernelGGL((k_mix_strip<E, KK>), grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only)
+    const dim3 grid((unsigned)n_strips), block(4 * kWave);              // 4 waves per strip
+#define NIIDMIX_STRIP(E, KK) hipLaunchKernelGGL((k_mix_strip<E, KK, 4>), grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only)
 #define NIIDMIX_STRIP_K(E) do { if (k == 3) NIIDMIX_STRIP(E, 3); else if (k == 5) NIIDMIX_STRIP(E, 5); else NIIDMIX_STRIP(E, 8); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_STRIP_K(true); else NIIDMIX_STRIP_K(false);
 #undef NIIDMIX_STRIP_K
