@@ -98,8 +98,10 @@ def parse():
     ap.add_argument("--hipmalloc-slabs", action="store_true",
                     help="single GPU: allocate the slabs with torch's default (hipMalloc) allocator "
                          "instead of the VMM-mapped slab pool")
-    ap.add_argument("--ld-pad", type=int, default=0,
-                    help="single GPU: pad every slab row by this many floats (ld = P + pad)")
+    ap.add_argument("--ld-pad", type=int, default=-1,
+                    help="single GPU: pad every slab row by this many floats (ld = P + pad); "
+                         "default: a 256-B row pitch for few-node low-degree graphs (ring 100), "
+                         "none otherwise")
     ap.add_argument("--workload", default="mix", choices=["mix", "grad-clique"],
                     help="mix: the headline neighbour mixing round; grad-clique: the --clique-gradient "
                          "gradient mean (k_grad_segment_mean) over the same 1000-node d-cliques "
@@ -812,7 +814,10 @@ def main():
         n_local = n_total = csr.n
         parallelism = "single GPU"
         gen = torch.Generator(device=dev).manual_seed(args.seed)
-        ld = p + args.ld_pad
+        # few nodes with ELL rows (ring 100): rows on a 256-B pitch, where the column-strip kernel
+        # (Mixer.kernel_for) stores whole cache lines (--ld-pad N: ld = p + N instead)
+        few = args.workload == "mix" and mixer.n <= ops.STRIP_MAX_ROWS and mixer.ell is not None
+        ld = p + args.ld_pad if args.ld_pad >= 0 else (-(-p // 64) * 64 if few else p)
         # node-state slabs in VMM-mapped HBM (niidmix.memory); --hipmalloc-slabs:
         # torch's default allocator instead (placement-dependent speed, for comparison)
         alloc = (lambda: torch.empty(n_local, ld, device=dev)) if args.hipmalloc_slabs else \
@@ -920,7 +925,9 @@ def main():
     slab_layout = (f"column-blocked [{xa.shape[0]}, {xa.shape[1]}, {xa.shape[2]}], "
                    f"{row_order} rows" if xa.dim() == 3 and (blocked or args.shard == "stripes") else
                    "window-blocked [K, rows_in, w]" if xa.dim() == 3 else
-                   "row-major [N, P]" + (f", {row_order} rows" if row_order != "rank" else ""))
+                   "row-major [N, P]" + (f" on a {xa.stride(0) * 4}-B row pitch"
+                                         if xa.dim() == 2 and xa.stride(0) != p else "")
+                   + (f", {row_order} rows" if row_order != "rank" else ""))
     single = None
     if world > 1 and args.single_ref != "off":
         # the N=1 point of this line, measured in the same run on rank 0's GPU with the same

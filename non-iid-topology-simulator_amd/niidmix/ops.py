@@ -812,6 +812,14 @@ class Mixer:
                            self.plan.max_clique_res)
         return out
 
+    def _strip_ok(self, x, out):
+        """The column-strip kernel (few nodes, ELL rows) on slabs whose rows sit on a 256-B pitch:
+        ring 100 at P = 62 006 13.7 us per round vs 15.0 for the band kernel on the same pitch; on
+        ld = P (rows at 216-B offsets) the three kernels are equal, 15.6-16 us (band_probe)."""
+        return (self.ell is not None and self.n <= STRIP_MAX_ROWS and x is not None and
+                x.dim() == 2 and x.shape[0] >= self.n and x.stride(0) % 64 == 0 and
+                (out is None or (out.dim() == 2 and out.stride(0) % 64 == 0)))
+
     def kernel_for(self, mode="fast", x=None, out=None):
         if mode == "exact":
             # measured on the 1000-node d-cliques round (P = 2^20): LDS-staged tiles 4.8 ms, global
@@ -821,6 +829,8 @@ class Mixer:
                 return "tile-lds-exact"
             if self.tile is not None:
                 return "tile-exact"
+            if self._strip_ok(x, out):
+                return "strip-exact"
             if self.band is not None and (x is None or (x.shape[0] == self.n and _lds_ok(x))) \
                     and (out is None or _lds_ok(out)):
                 return "band-exact"
@@ -832,6 +842,8 @@ class Mixer:
         if self.plan is not None and self.tlds is not None and (x is None or _lds_ok(x)) and \
                 (out is None or _lds_ok(out)):
             return "tile-lds-fast"               # clique graph with removed edges
+        if self._strip_ok(x, out):
+            return "strip-fast"
         if self.band is not None and (x is None or (x.shape[0] == self.n and _lds_ok(x))) \
                 and (out is None or _lds_ok(out)):
             return "band-fast"

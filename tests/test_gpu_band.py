@@ -206,3 +206,30 @@ def test_strip_sizes_vs_ell(n, k, p, gpu, oracle_mod):
             ops.mix_strip(big, torch.zeros(257 * 3, dtype=torch.int32, device=gpu),
                           torch.zeros(257 * 3, device=gpu), torch.ones(257, dtype=torch.int32, device=gpu),
                           torch.empty_like(big), 3, ops.EXACT)
+
+
+def test_strip_auto_on_row_pitch(gpu):
+    """Ring 100 at P = 62 006 as bench.py allocates it (rows on a 256-B pitch): the Mixer picks the
+    strip kernel (on ld = P it keeps ELL / band), bitwise the ELL kernel over two ping-pong rounds
+    captured in a hipGraph, and the padding columns are never written."""
+    from bench import golden
+    from niidmix import ops
+    csr, _ = golden("ring100_p257")
+    m = ops.Mixer(csr=csr, device=gpu)
+    n, p, ld = csr.n, 62006, 62016
+    pa = torch.full((n, ld), 7.0, device=gpu)
+    pb = torch.full((n, ld), 7.0, device=gpu)
+    xa, xb = pa[:, :p], pb[:, :p]
+    xa.normal_(generator=torch.Generator(device=gpu).manual_seed(3))
+    assert m.kernel_for("exact", xa, xb) == "strip-exact" and m.kernel_for("fast", xa, xb) == "strip-fast"
+    assert m.kernel_for("exact", xa.contiguous()) in ("ell-exact", "band-exact")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m(xa, out=xb, mode="exact")
+        m(xb, out=xa, mode="exact")
+    x0 = xa.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    ref = m(m(x0.contiguous(), kernel="ell-exact"), kernel="ell-exact")
+    assert torch.equal(xa, ref)
+    assert bool((pa[:, p:] == 7.0).all()) and bool((pb[:, p:] == 7.0).all())

@@ -70,6 +70,17 @@ def main():
     for mode, kname in (("fast", "strip-fast"), ("exact", "strip-exact")):
         us = graph_round_us(lambda x, y: mr(x, out=y, kernel=kname), xa, xb, a.steps, a.reps)
         print(f"strip {mode:5s}       {us[0]:7.2f} / {us[1]:7.2f} us per round (column strips in LDS)")
+    # rows on a 256-B pitch (ld = p rounded up to 64 floats): every wave's 256-B row piece is then
+    # whole cache lines (ld = p = 62 006 floats puts row r at 216 r mod 256 B)
+    ldp = -(-p // 64) * 64
+    pa = torch.empty((n, ldp), device=dev)
+    pa[:, :p].copy_(xa)
+    pb = torch.empty((n, ldp), device=dev)
+    va, vb = pa[:, :p], pb[:, :p]
+    for kname in ("strip-fast", "band-fast", "ell-fast"):
+        mm = m if kname == "ell-fast" else mr
+        us = graph_round_us(lambda x, y: mm(x, out=y, kernel=kname), va, vb, a.steps, a.reps)
+        print(f"{kname:10s} ld={ldp} {us[0]:7.2f} / {us[1]:7.2f} us per round (256-B row pitch)")
     # the strip kernel's result against the band kernel's (exact: bitwise)
     ya, yb = torch.empty_like(xa), torch.empty_like(xa)
     mr(xa, out=ya, kernel="band-exact")
