@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 // through L2).  The descriptors of a wave's rows are loaded lane-parallel with the strip (lane i:
 // row w + SW i) and handed out by v_readlane: no scalar-load round trip per row.  Same arithmetic,
 // in the same order, as k_mix_ell (z from the row's first entry, self).
-template <bool EXACT, int K, int SW>
+template <bool EXACT, int K, int SW, int SV>
 __global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__ x, int64_t ld_x,
                                                        float *__restrict__ y, int64_t ld_y,
                                                        int n_rows, int64_t p,
@@ -376,18 +376,27 @@ __global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__
                                                        const float *__restrict__ ell_val,
                                                        const int32_t *__restrict__ ell_len,
                                                        int avg_only) {
-    extern __shared__ float strip[];          // [n_rows][64]
+    // SV columns per lane: 1 (any slab), or 4 (rows on a 16-B pitch with room for a lane's whole
+    // float4 past p, niidmix_mix_strip_f32): 256-column strips, one 1 KiB LDS-DMA per row
+    typedef float fv __attribute__((ext_vector_type(SV)));
+    extern __shared__ float strip[];          // [n_rows][64 * SV]
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) void glb_void;
+    constexpr int RW = kWave * SV;            // floats per staged row
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = wave_id();
-    const int64_t c0 = (int64_t)blockIdx.x * kWave;
-    const int64_t col = c0 + lane;
-    const bool ok = col < p;
-    const float *xs = x + (ok ? col : c0);    // lanes past p read a valid column, store nothing
-    for (int r = wave; r < n_rows; r += SW)
-        __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
-                                         (lds_void *)(strip + r * kWave), 4, 0, 0);
+    const int64_t c0 = (int64_t)blockIdx.x * RW;
+    const int64_t col = c0 + SV * lane;
+    const bool any = col < p;                 // this lane stores some columns
+    const float *xs = x + (any ? col : c0);   // lanes past p read valid columns, store nothing
+    for (int r = wave; r < n_rows; r += SW) {
+        if constexpr (SV == 4)
+            __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
+                                             (lds_void *)(strip + r * RW), 16, 0, 0);
+        else
+            __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
+                                             (lds_void *)(strip + r * RW), 4, 0, 0);
+    }
     const int mr = wave + SW * lane;          // the row this lane describes (n_rows <= 64 SW)
     const bool in = mr < n_rows;
     const int dlen = in ? ell_len[mr] : 0;
@@ -405,18 +414,32 @@ __global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__
     for (int i = 0; i < nw; ++i) {
         const int r = wave + SW * i;
         const int len = __builtin_amdgcn_readlane(dlen, i);
-        float xv[K];
+        fv xv[K];
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            xv[j] = strip[__builtin_amdgcn_readlane(dcol[j < len ? j : 0], i) * kWave + lane];
-        const float z = xv[0] * 0.f;          // self * 0 (d_sgd.py:105: self is entry 0)
-        float acc = z;
+            xv[j] = *reinterpret_cast<const fv *>(
+                strip + __builtin_amdgcn_readlane(dcol[j < len ? j : 0], i) * RW + SV * lane);
+        fv z, acc;
+#pragma unroll
+        for (int e = 0; e < SV; ++e) { z[e] = xv[0][e] * 0.f; acc[e] = z[e]; }   // self * 0
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            if (j < len)                                                   // wave-uniform
-                acc = axpy<EXACT>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dval[j]), i)),
-                                  xv[j], acc);
-        if (ok) __builtin_nontemporal_store(avg_only ? acc : z + acc, dst + (int64_t)r * ld_y);
+            if (j < len) {                                                 // wave-uniform
+                const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dval[j]), i));
+#pragma unroll
+                for (int e = 0; e < SV; ++e) acc[e] = axpy<EXACT>(w, xv[j][e], acc[e]);
+            }
+        fv o;
+#pragma unroll
+        for (int e = 0; e < SV; ++e) o[e] = avg_only ? acc[e] : z[e] + acc[e];
+        float *d = dst + (int64_t)r * ld_y;
+        if (col + SV <= p) {
+            __builtin_nontemporal_store(o, reinterpret_cast<fv *>(d));
+        } else if (any) {
+#pragma unroll
+            for (int e = 0; e < SV; ++e)
+                if (col + e < p) __builtin_nontemporal_store(o[e], d + e);
+        }
     }
 }
 
@@ -3653,14 +3676,29 @@ int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     if (reinterpret_cast<uintptr_t>(x) & 3) return set_error(NIIDMIX_EUNSUPPORTED, "x not 4-B aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int64_t n_strips = (p + kWave - 1) / kWave;
+    // float4 lanes (256-column strips, 1 KiB per staged row) when every lane's float4 stays inside
+    // its row (ld >= p rounded up to 4) and the rows sit on 16-B boundaries, and the strip fits
+    // 156 KB of LDS; else one float per lane (64-column strips).  NIIDMIX_STRIP_SV=1 forces the
+    // latter (tuning)
+    const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
+    int sv = (ld_x % 4 == 0 && ld_y % 4 == 0 && (al & 15) == 0 && ld_x >= (p + 3) / 4 * 4 &&
+              n_rows <= 156) ? 4 : 1;
+    if (const char *e = getenv("NIIDMIX_STRIP_SV")) if (atoi(e) == 1) sv = 1;
+    const int64_t n_strips = (p + kWave * sv - 1) / (kWave * sv);
     if (n_strips > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many strips");
-    const size_t lds = (size_t)n_rows * kWave * sizeof(float);        // <= 64 KB
+    const size_t lds = (size_t)n_rows * kWave * sv * sizeof(float);   // <= 156 KB
     const dim3 grid((unsigned)n_strips), block(4 * kWave);              // 4 waves per strip
-#define NIIDMIX_STRIP(E, KK) hipLaunchKernelGGL((k_mix_strip<E, KK, 4>), grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only)
-#define NIIDMIX_STRIP_K(E) do { if (k == 3) NIIDMIX_STRIP(E, 3); else if (k == 5) NIIDMIX_STRIP(E, 5); else NIIDMIX_STRIP(E, 8); } while (0)
+#define NIIDMIX_STRIP(E, KK, V) do { \
+        auto kfn = k_mix_strip<E, KK, 4, V>; \
+        if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+            return set_error(NIIDMIX_EHIP, "k_mix_strip: %zu B of LDS refused", lds); \
+        hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only); \
+    } while (0)
+#define NIIDMIX_STRIP_V(E, KK) do { if (sv == 4) NIIDMIX_STRIP(E, KK, 4); else NIIDMIX_STRIP(E, KK, 1); } while (0)
+#define NIIDMIX_STRIP_K(E) do { if (k == 3) NIIDMIX_STRIP_V(E, 3); else if (k == 5) NIIDMIX_STRIP_V(E, 5); else NIIDMIX_STRIP_V(E, 8); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_STRIP_K(true); else NIIDMIX_STRIP_K(false);
 #undef NIIDMIX_STRIP_K
+#undef NIIDMIX_STRIP_V
 #undef NIIDMIX_STRIP
     return check_launch("k_mix_strip");
 }

@@ -41,7 +41,10 @@ def test_band_vs_reference_golden(name, gpu, oracle_mod):
         assert oracle_mod.bitwise_equal(mr(xp, mode="exact")[pt].cpu().numpy(), g["y"])
         p -= 1                            # ... and its first 256 columns the band kernel
     xe = xp[:, :p].contiguous()
-    assert mr.kernel_for("exact", xe) == "band-exact" and mr.kernel_for("fast", xe) == "band-fast"
+    # p = 256: rows on a 256-B pitch, where the strip kernel is the auto choice (few nodes); the
+    # band kernel is called explicitly below
+    assert mr.kernel_for("exact", xe) in ("band-exact", "strip-exact")
+    assert mr.kernel_for("fast", xe) in ("band-fast", "strip-fast")
     y = mr(xe, kernel="band-exact")[pt].cpu().numpy()
     assert oracle_mod.bitwise_equal(y, g["y"][:, :p])
     yf = mr(xe, kernel="band-fast")[pt].cpu().numpy()
@@ -195,6 +198,16 @@ def test_strip_sizes_vs_ell(n, k, p, gpu, oracle_mod):
     y = m(x, kernel="strip-exact").cpu().numpy()
     ref = oracle_mod.mix_exact_c(wide.cpu().numpy(), csr.row_ptr, csr.col, csr.val, cols=(3, 3 + p))
     assert oracle_mod.bitwise_equal(y, ref[:, 3:3 + p])
+    # contiguous rows (float4 lanes when p % 4 == 0: 256-column strips), and a 16-B row pitch
+    yc = m(x.contiguous(), kernel="strip-exact").cpu().numpy()
+    assert oracle_mod.bitwise_equal(yc, ref[:, 3:3 + p])
+    ld = -(-p // 64) * 64
+    xp = torch.empty((n, ld), device=gpu)
+    xp[:, :p].copy_(x)
+    outp = torch.full((n, ld), 5.0, device=gpu)
+    m(xp[:, :p], out=outp[:, :p], kernel="strip-exact")
+    assert oracle_mod.bitwise_equal(outp[:, :p].cpu().numpy(), ref[:, 3:3 + p])
+    assert bool((outp[:, p:] == 5.0).all())
     out = torch.empty((n, p), device=gpu)
     ops.mix_strip(x.contiguous(), m.e_col, m.e_val, m.e_len, out, m.ell, ops.EXACT | ops.AVERAGE_ONLY)
     ref_avg = torch.empty_like(out)
