@@ -3687,19 +3687,24 @@ int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     const int64_t n_strips = (p + kWave * sv - 1) / (kWave * sv);
     if (n_strips > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many strips");
     const size_t lds = (size_t)n_rows * kWave * sv * sizeof(float);   // <= 156 KB
-    const dim3 grid((unsigned)n_strips), block(4 * kWave);              // 4 waves per strip
-#define NIIDMIX_STRIP(E, KK, V) do { \
-        auto kfn = k_mix_strip<E, KK, 4, V>; \
+    // waves per strip: 8 (NIIDMIX_STRIP_SW = 4 / 8 / 16 overrides, tuning)
+    int sw = 8;
+    if (const char *e = getenv("NIIDMIX_STRIP_SW")) { const int v = atoi(e); if (v == 4 || v == 8 || v == 16) sw = v; }
+    const dim3 grid((unsigned)n_strips), block(sw * kWave);
+#define NIIDMIX_STRIP_W(E, KK, V, W) do { \
+        auto kfn = k_mix_strip<E, KK, W, V>; \
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_strip: %zu B of LDS refused", lds); \
         hipLaunchKernelGGL(kfn, grid, block, lds, s, x, ld_x, y, ld_y, (int)n_rows, p, ell_col, ell_val, ell_len, avg_only); \
     } while (0)
+#define NIIDMIX_STRIP(E, KK, V) do { if (sw == 4) NIIDMIX_STRIP_W(E, KK, V, 4); else if (sw == 8) NIIDMIX_STRIP_W(E, KK, V, 8); else NIIDMIX_STRIP_W(E, KK, V, 16); } while (0)
 #define NIIDMIX_STRIP_V(E, KK) do { if (sv == 4) NIIDMIX_STRIP(E, KK, 4); else NIIDMIX_STRIP(E, KK, 1); } while (0)
 #define NIIDMIX_STRIP_K(E) do { if (k == 3) NIIDMIX_STRIP_V(E, 3); else if (k == 5) NIIDMIX_STRIP_V(E, 5); else NIIDMIX_STRIP_V(E, 8); } while (0)
     if (mode == NIIDMIX_MODE_EXACT) NIIDMIX_STRIP_K(true); else NIIDMIX_STRIP_K(false);
 #undef NIIDMIX_STRIP_K
 #undef NIIDMIX_STRIP_V
 #undef NIIDMIX_STRIP
+#undef NIIDMIX_STRIP_W
     return check_launch("k_mix_strip");
 }
 

@@ -814,8 +814,8 @@ class Mixer:
 
     def _strip_ok(self, x, out):
         """The column-strip kernel (few nodes, ELL rows) on slabs whose rows sit on a 256-B pitch:
-        ring 100 at P = 62 006 13.7 us per round vs 15.0 for the band kernel on the same pitch; on
-        ld = P (rows at 216-B offsets) the three kernels are equal, 15.6-16 us (band_probe)."""
+        ring 100 at P = 62 006 11.0 us per round vs 14.8 for the band kernel on the same pitch; on
+        ld = P (rows at 216-B offsets) the kernels are equal, 15.6-16 us (tools/band_probe.py)."""
         return (self.ell is not None and self.n <= STRIP_MAX_ROWS and x is not None and
                 x.dim() == 2 and x.shape[0] >= self.n and x.stride(0) % 64 == 0 and
                 (out is None or (out.dim() == 2 and out.stride(0) % 64 == 0)))

@@ -81,6 +81,14 @@ def main():
         mm = m if kname == "ell-fast" else mr
         us = graph_round_us(lambda x, y: mm(x, out=y, kernel=kname), va, vb, a.steps, a.reps)
         print(f"{kname:10s} ld={ldp} {us[0]:7.2f} / {us[1]:7.2f} us per round (256-B row pitch)")
+    for sv in ("4", "1"):
+        for sw in ("4", "8", "16"):
+            os.environ["NIIDMIX_STRIP_SV"], os.environ["NIIDMIX_STRIP_SW"] = sv, sw
+            us = graph_round_us(lambda x, y: mr(x, out=y, kernel="strip-fast"), va, vb, a.steps,
+                                a.reps)
+            print(f"strip SV={sv} SW={sw:2s} ld={ldp} {us[0]:7.2f} / {us[1]:7.2f} us per round")
+    os.environ.pop("NIIDMIX_STRIP_SV")
+    os.environ.pop("NIIDMIX_STRIP_SW")
     # the strip kernel's result against the band kernel's (exact: bitwise)
     ya, yb = torch.empty_like(xa), torch.empty_like(xa)
     mr(xa, out=ya, kernel="band-exact")
