@@ -30,7 +30,7 @@ one exact k_mix_tile_lds 8388608000 --kernel tile-lds-exact --steps 10 || exit 5
 one fc1000 k_mix_bigclique 8388608000 --config fc1000 --steps 10 || exit 5
 one d10k k_mix_clique 83886080000 --config dcliques10000 --steps 5 --warmup 2 || exit 5
 one d10k_exact k_mix_tile_lds 83886080000 --config dcliques10000 --kernel tile-lds-exact --steps 3 --warmup 1 || exit 5
-one ring100 k_mix_band 49604800 --config ring100 --steps 200 || exit 5
+one ring100 k_mix_strip 49604800 --config ring100 --steps 200 || exit 5
 one grad k_grad_segment_mean 8388608000 --workload grad-clique --steps 10 || exit 5
 one dense k_mix_dense 8388608000 --config fc1000 --kernel dense --steps 3 --warmup 1 || exit 5
 timeout -k 10 900 python bench.py --no-cpu-baseline --e2e --e2e-step --steps 3 > $O/bench_e2e.json 2> $O/bench_e2e.err || { echo e2e failed; tail $O/bench_e2e.err; exit 6; }
