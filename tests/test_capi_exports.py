@@ -121,3 +121,12 @@ def test_argument_errors_without_gpu():
     assert E(16, 4, 1024, 4, 1, 4, 4, 8, 8, 8, 0, None) == _lib.EINVAL                  # unpadded width
     assert E(16, 4, 16, 4, 1, 4, 3, 8, 8, 8, 0, None) == _lib.EALIAS
     assert E(None, 4, 1024, 4, 1, 4, 3, 8, 8, 8, 0, None) == _lib.EINVAL
+    S = L.niidmix_mix_strip_f32
+    assert S(16, 64, 1 << 30, 64, 2, 64, 4, 8, 8, 8, 0, None) == _lib.EUNSUPPORTED     # ELL width 4
+    assert S(16, 64, 1 << 30, 64, 257, 64, 3, 8, 8, 8, 0, None) == _lib.EUNSUPPORTED   # > 256 rows
+    assert S(16, 64, 16 + 4 * 64, 64, 2, 64, 3, 8, 8, 8, 0, None) == _lib.EALIAS       # y = x's row 1
+    assert S(None, 64, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 0, None) == _lib.EINVAL
+    assert S(16, 32, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 0, None) == _lib.EINVAL          # ld_x < p
+    assert S(18, 64, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 0, None) == _lib.EUNSUPPORTED     # x not 4-B aligned
+    assert S(16, 64, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 16, None) == _lib.EINVAL         # unknown mode
+    assert S(16, 64, 1 << 30, 64, 0, 64, 3, 8, 8, 8, 0, None) == _lib.OK              # no rows
