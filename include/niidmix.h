@@ -131,10 +131,12 @@ int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
                          int64_t p, int k, int band, const int32_t *ell_col, const float *ell_val,
                          const int32_t *ell_len, int mode, void *stream);
 
-/* The same round for FEW nodes (n_rows <= 256; ring 100, BASELINE configs[1]) by column strips:
- * one wave owns 64 columns of every row, stages them in LDS (n_rows x 256 B) and combines each
- * output row from there in its ELL order, so each element of x is read from memory once and a
- * round is one generation of ceil(p / 64) waves.  Any row order.  Descriptors: the ELL arrays of
+/* The same round (d_sgd.average, tools/simulate/algorithm/d_sgd.py:96-116) for FEW nodes
+ * (n_rows <= 256; ring 100, BASELINE configs[1], tools/setup/topology/ring.py:12-27) by column
+ * strips: a block of 8 waves owns a strip of every row -- 256 columns (float4 lanes) when x and y
+ * are 16-B aligned, both ld are multiples of 4, ld_x >= p rounded up to 4 and n_rows <= 156, else
+ * 64 columns -- stages it in LDS by LDS-DMA and combines each output row from there in its ELL
+ * order, so each element of x is read from memory once.  Any row order.  Descriptors: the ELL arrays of
  * niidmix_mix_ell_f32 (k = 3, 5 or 8).  x 4-B aligned; x and y: [n_rows, ld].  mode as
  * niidmix_mix_ell_f32; bit-identical to it (and to niidmix_mix_csr_f32) in EXACT mode.  Round 4
  * (ABI 4). */
