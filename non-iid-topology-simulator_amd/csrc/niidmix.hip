@@ -1107,16 +1107,16 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 // the compiler's own schedule waited for four fresh LDS reads before every group of four MFMAs
 // (MfmaUtil 74 %).  Tried and slower: k-contiguous LDS tiles read as ds_read_b128 with per-lane
 // dword global loads (20.9 ms), and a branch-free clamped fetch (19.0 ms), vs 18.05 ms.
-template <bool VEC, bool AVEC, bool SCHED = false>
-__global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
+template <bool VEC, bool AVEC, bool SCHED = false, int BK = kDBK, int OCC = (BK == 32 ? 2 : 3)>
+__global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict__ x, int64_t ld_x,
                                                       float *__restrict__ y, int64_t ld_y, int64_t n,
                                                       int64_t p, const float *__restrict__ w,
                                                       int64_t n_it, int64_t n_items,
                                                       const int64_t *__restrict__ csr_ptr,
                                                       const int32_t *__restrict__ csr_col,
                                                       const float *__restrict__ csr_val) {
-    __shared__ float As[2][kDBK][kDBM + kDPad];
-    __shared__ float Bs[2][kDBK][kDBN + kDPad];
+    __shared__ float As[2][BK][kDBM + kDPad];
+    __shared__ float Bs[2][BK][kDBN + kDPad];
     const int tid = threadIdx.x;
     const int wave = wave_id();
     const int lane = tid & 63;
@@ -1139,10 +1139,23 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-        float ra[4][4], rb[4][4];
+        constexpr int NH = BK / 8;           // float4 rows per thread per operand
+        float ra[NH][4], rb[NH][4];
+        // interior tiles and K-steps (block-uniform): no per-lane bounds, no zero-fill
+        const bool inner = AVEC && VEC && i0 + kDBM <= n && j0 + kDBN <= p;
         auto fetch = [&](int64_t k0) {
+            if (inner && k0 + BK <= n) {
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
+                for (int h = 0; h < NH; ++h) {
+                    const int64_t kr = k0 + lk + 8 * h;
+                    const float4 a = ld4(w + kr * n + i0 + lc), b = ld4(x + kr * ld_x + j0 + lc);
+                    ra[h][0] = a.x; ra[h][1] = a.y; ra[h][2] = a.z; ra[h][3] = a.w;
+                    rb[h][0] = b.x; rb[h][1] = b.y; rb[h][2] = b.z; rb[h][3] = b.w;
+                }
+                return;
+            }
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
                 const int64_t kr = k0 + lk + 8 * h;
                 if (AVEC) {
                     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1171,20 +1184,20 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
         };
         fetch(0);
         int buf = 0;
-        for (int64_t k0 = 0; k0 < n; k0 += kDBK) {
+        for (int64_t k0 = 0; k0 < n; k0 += BK) {
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
+            for (int h = 0; h < NH; ++h) {
                 *reinterpret_cast<float4 *>(&As[buf][lk + 8 * h][lc]) = make_float4(ra[h][0], ra[h][1], ra[h][2], ra[h][3]);
                 *reinterpret_cast<float4 *>(&Bs[buf][lk + 8 * h][lc]) = make_float4(rb[h][0], rb[h][1], rb[h][2], rb[h][3]);
             }
             __syncthreads();
-            if (k0 + kDBK < n) fetch(k0 + kDBK);          // in flight during the MFMAs below
+            if (k0 + BK < n) fetch(k0 + BK);          // in flight during the MFMAs below
             if (SCHED) {
                 // every operand read written first, then the MFMAs; the scheduling groups below
                 // interleave them so the reads of step u + 2 are in flight during step u's MFMAs
-                float a0v[kDBK / 2], a1v[kDBK / 2], b0v[kDBK / 2], b1v[kDBK / 2];
+                float a0v[BK / 2], a1v[BK / 2], b0v[BK / 2], b1v[BK / 2];
 #pragma unroll
-                for (int u = 0; u < kDBK / 2; ++u) {
+                for (int u = 0; u < BK / 2; ++u) {
                     const int kq = 2 * u + (lane >> 5);
                     a0v[u] = As[buf][kq][wm * 64 + (lane & 31)];
                     a1v[u] = As[buf][kq][wm * 64 + 32 + (lane & 31)];
@@ -1192,7 +1205,7 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
                     b1v[u] = Bs[buf][kq][wn * 64 + 32 + (lane & 31)];
                 }
 #pragma unroll
-                for (int u = 0; u < kDBK / 2; ++u) {
+                for (int u = 0; u < BK / 2; ++u) {
                     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0v[u], b0v[u], acc[0][0], 0, 0, 0);
                     acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0v[u], b1v[u], acc[0][1], 0, 0, 0);
                     acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1v[u], b0v[u], acc[1][0], 0, 0, 0);
@@ -1200,14 +1213,14 @@ __global__ __launch_bounds__(256, 2) void k_mix_dense(const float *__restrict__ 
                 }
                 __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);          // DS reads, steps 0-1
 #pragma unroll
-                for (int u = 0; u < kDBK / 2 - 2; ++u) {
+                for (int u = 0; u < BK / 2 - 2; ++u) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);      // MFMAs of step u
                     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);      // DS reads of step u + 2
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
             } else {
 #pragma unroll
-            for (int kk = 0; kk < kDBK; kk += 2) {
+            for (int kk = 0; kk < BK; kk += 2) {
                 const int kq = kk + (lane >> 5);
                 const float a0 = As[buf][kq][wm * 64 + (lane & 31)];
                 const float a1 = As[buf][kq][wm * 64 + 32 + (lane & 31)];
@@ -3870,6 +3883,18 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     // vectorised operands: the interleaved DS-read / MFMA schedule (18.05 vs 18.87 ms on FC-1000);
     // NIIDMIX_DENSE_SCHED=0 restores the compiler's schedule (tuning)
     const char *sc = getenv("NIIDMIX_DENSE_SCHED");
+    // K-steps of 16 (168 VGPRs, half the LDS: three blocks per CU) 17.2 vs 18.0 ms with 32 (256
+    // VGPRs, two blocks; NIIDMIX_DENSE_BK=32 restores it, =8 and NIIDMIX_DENSE_OCC=4: tuning)
+    const char *bk = getenv("NIIDMIX_DENSE_BK");
+    const char *oc = getenv("NIIDMIX_DENSE_OCC");
+    const int bkv = bk ? atoi(bk) : 16, occ = oc ? atoi(oc) : 0;
+    if (vec && avec && !(sc && sc[0] == '0') && (bkv == 16 || bkv == 8)) {
+#define NIIDMIX_DENSE_T(B, O) hipLaunchKernelGGL((k_mix_dense<true, true, true, B, O>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items, row_ptr, col, val)
+        if (bkv == 16) { if (occ == 4) NIIDMIX_DENSE_T(16, 4); else NIIDMIX_DENSE_T(16, 3); }
+        else { if (occ == 4) NIIDMIX_DENSE_T(8, 4); else NIIDMIX_DENSE_T(8, 3); }
+#undef NIIDMIX_DENSE_T
+        return check_launch("k_mix_dense");
+    }
     if (vec && avec && !(sc && sc[0] == '0')) {
         hipLaunchKernelGGL((k_mix_dense<true, true, true>), grid, block, 0, s, x, ld_x, y, ld_y, n, p, w, n_it, n_items, row_ptr, col, val);
         return check_launch("k_mix_dense");
