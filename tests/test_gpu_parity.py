@@ -450,6 +450,33 @@ def test_fc1000_dense_and_factored(kernel, gpu, oracle_mod):
     assert ok, worst
 
 
+def test_dense_kstep_variants_agree(gpu, oracle_mod, monkeypatch):
+    """The dense MFMA kernel's K-step / occupancy variants (16 shipped; 32 = round 3; 8 and four
+    waves per SIMD: tuning switches) accumulate k in the same order, so on finite inputs their
+    outputs are bitwise equal, and within the tolerance of the oracle; ragged M, K and P tiles
+    (N = 1000, P = 4096 + 12), interior tiles through the unchecked fetch."""
+    from niidmix.topology import mh_csr
+    n = 1000
+    edges = {i: [j for j in range(n) if j != i] for i in range(n)}
+    csr = mh_csr(n, edges)
+    ops = _ops()
+    m = ops.Mixer(csr=csr, device=gpu)
+    x = torch.randn(n, 4096 + 12, device=gpu)
+    outs = {}
+    for bk, occ in (("16", "3"), ("32", "0"), ("8", "3"), ("8", "4"), ("16", "4")):
+        monkeypatch.setenv("NIIDMIX_DENSE_BK", bk)
+        monkeypatch.setenv("NIIDMIX_DENSE_OCC", occ)
+        outs[(bk, occ)] = m(x, kernel="dense").cpu().numpy()
+    base = outs[("16", "3")]
+    for k, y in outs.items():
+        assert oracle_mod.bitwise_equal(y, base), k
+    xn = x.cpu().numpy()
+    ref = oracle_mod.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle_mod.check_tolerance(base, ref, bound, rtol=RTOL)
+    assert ok, worst
+
+
 @pytest.mark.gpu
 def test_stream_copy(gpu):
     """The bench's copy-ceiling primitive copies exactly (ragged tail of the last block included)."""
