@@ -246,3 +246,27 @@ def test_strip_auto_on_row_pitch(gpu):
     ref = m(m(x0.contiguous(), kernel="ell-exact"), kernel="ell-exact")
     assert torch.equal(xa, ref)
     assert bool((pa[:, p:] == 7.0).all()) and bool((pb[:, p:] == 7.0).all())
+
+
+def test_strip_wave_and_lane_variants(gpu, monkeypatch):
+    """The strip kernel's tuning switches (4 / 8 / 16 waves per strip, one-float lanes forced) give
+    the shipped kernel's result bitwise, exact and fast, on ring 100 at P = 62 006 on a 256-B row
+    pitch (float4 lanes by default)."""
+    from bench import golden
+    from niidmix import ops
+    csr, _ = golden("ring100_p257")
+    m = ops.Mixer(csr=csr, device=gpu)
+    n, p, ld = csr.n, 62006, 62016
+    xp = torch.empty((n, ld), device=gpu)
+    x = xp[:, :p]
+    x.normal_(generator=torch.Generator(device=gpu).manual_seed(5))
+    for kname in ("strip-exact", "strip-fast"):
+        base = m(x, kernel=kname)
+        for sw, sv in (("4", "4"), ("16", "4"), ("8", "1"), ("4", "1")):
+            monkeypatch.setenv("NIIDMIX_STRIP_SW", sw)
+            monkeypatch.setenv("NIIDMIX_STRIP_SV", sv)
+            assert torch.equal(m(x, kernel=kname), base), (kname, sw, sv)
+        monkeypatch.delenv("NIIDMIX_STRIP_SW")
+        monkeypatch.delenv("NIIDMIX_STRIP_SV")
+    ref = m(x.contiguous(), kernel="ell-exact")
+    assert torch.equal(m(x, kernel="strip-exact"), ref)
