@@ -368,6 +368,10 @@ __global__ __launch_bounds__(256) void k_mix_ell(const float *__restrict__ x, in
 // through L2).  The descriptors of a wave's rows are loaded lane-parallel with the strip (lane i:
 // row w + SW i) and handed out by v_readlane: no scalar-load round trip per row.  Same arithmetic,
 // in the same order, as k_mix_ell (z from the row's first entry, self).
+#ifndef NIIDMIX_STRIP_AUX
+#define NIIDMIX_STRIP_AUX 2   // cache policy of the strip's LDS-DMA loads: nt (each element is read
+                              // once): ring 100 9.8-9.9 vs 10.7-10.8 us with 0 (tuning builds: -D)
+#endif
 template <bool EXACT, int K, int SW, int SV>
 __global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__ x, int64_t ld_x,
                                                        float *__restrict__ y, int64_t ld_y,
@@ -392,10 +396,10 @@ __global__ __launch_bounds__(64 * SW) void k_mix_strip(const float *__restrict__
     for (int r = wave; r < n_rows; r += SW) {
         if constexpr (SV == 4)
             __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
-                                             (lds_void *)(strip + r * RW), 16, 0, 0);
+                                             (lds_void *)(strip + r * RW), 16, 0, NIIDMIX_STRIP_AUX);
         else
             __builtin_amdgcn_global_load_lds((glb_void *)(xs + (int64_t)r * ld_x),
-                                             (lds_void *)(strip + r * RW), 4, 0, 0);
+                                             (lds_void *)(strip + r * RW), 4, 0, NIIDMIX_STRIP_AUX);
     }
     const int mr = wave + SW * lane;          // the row this lane describes (n_rows <= 64 SW)
     const bool in = mr < n_rows;
