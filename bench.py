@@ -546,6 +546,79 @@ def guarded_leg(fn, dist, world, rank, flag_device="cpu"):
     return info, None
 
 
+def world_identity(dev, dist, world, backend):
+    """What the N>1 run actually ran on: the backend, the RCCL version torch
+    links, the world size the process group reports, and each rank's device identity (GPU UUID and
+    PCI domain:bus:device, or the host process for the CPU rehearsals) all-gathered, so the line
+    itself shows N ranks on N distinct GPUs."""
+    import socket
+    if dev.type == "cuda":
+        pr = torch.cuda.get_device_properties(dev)
+        ident = {"uuid": str(getattr(pr, "uuid", "")),
+                 "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+                 "host": socket.gethostname(), "name": pr.name}
+    else:
+        ident = {"uuid": None, "pci": None, "host": socket.gethostname(),
+                 "name": f"cpu pid {os.getpid()}"}
+    ids = [None] * world
+    if dist is not None and world > 1:
+        dist.all_gather_object(ids, ident)
+    else:
+        ids = [ident]
+    keys = [(d["host"], d["uuid"], d["pci"]) if d["uuid"] else (d["host"], d["name"]) for d in ids]
+    version = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            version = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as e:                       # noqa: BLE001 - recorded, not fatal
+            version = f"unavailable: {e}"
+    return {"backend": backend, "rccl_version": version,
+            "world_size": dist.get_world_size() if dist is not None and world > 1 else 1,
+            "distinct_devices": len(set(keys)), "devices": ids}
+
+
+def exchange_rate(sm, x, rounds, dev, dist, backend):
+    """The node-shard halo exchange ALONE (no mixing): `rounds` rounds of every window's grouped
+    send/recv, timed on the host between device synchronisations and barriers.  Per rank: bytes
+    received and sent per round, seconds per round, and the achieved rate (received bytes / time)
+    all-gathered -- the xGMI GB/s each rank's links delivered."""
+    world = sm.world
+    cuda = dev.type == "cuda"
+    if world < 2:
+        return None
+    if cuda:
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        if cuda:
+            with torch.cuda.stream(sm.comm_stream):
+                pend = [sm.transport.exchange(sm, k, x[k]) for k in range(sm.k)]
+                for h in pend:
+                    sm.transport.wait(h)
+        else:
+            pend = [sm.transport.exchange(sm, k, x[k]) for k in range(sm.k)]
+            for h in pend:
+                sm.transport.wait(h)
+    if cuda:
+        torch.cuda.synchronize(dev)
+    sec = (time.perf_counter() - t0) / rounds
+    dist.barrier()
+    mine = torch.tensor([sm.halo_bytes, sm.send_bytes, sec], dtype=torch.float64,
+                        device=dev if (backend == "nccl" and cuda) else "cpu")
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    rows = [t.tolist() for t in allr]
+    return {"rounds": rounds,
+            "ms_per_round": [round(r[2] * 1e3, 4) for r in rows],
+            "recv_GB": [float(f"{r[0] / 1e9:.4g}") for r in rows],
+            "send_GB": [float(f"{r[1] / 1e9:.4g}") for r in rows],
+            "recv_GBs_per_rank": [float(f"{r[0] / r[2] / 1e9:.4g}") if r[2] > 0 else None
+                                  for r in rows],
+            "method": "exchange only (no mixing), host clock between device synchronisations"}
+
+
 def node_shard_leg(make, interclique, steps, warmup, dev, dist, backend, seed=0, single_ms=None,
                    fixed=False, fill=None):
     """Time the NODE-SHARD partition on one interclique with bench's own timed loop: `make(ic)`
@@ -588,6 +661,10 @@ def node_shard_leg(make, interclique, steps, warmup, dev, dist, backend, seed=0,
         key = "speedup_vs_1gpu" if fixed else "weak_efficiency_vs_1gpu"
         info[key] = round(single_ms / ms, 3)
     last = xa if (steps + warmup) % 2 == 0 else xb
+    if dist is not None and sm.world > 1:
+        # after the timed rounds, on the slab that is not the result: the exchange alone
+        info["xgmi"] = exchange_rate(sm, xb if last is xa else xa, max(2, steps // 2), dev, dist,
+                                     backend)
     return info, last, sm
 
 
@@ -791,6 +868,7 @@ def main():
             dist.init_process_group(backend, timeout=pg_timeout)
 
     from niidmix import memory, ops
+    ident = world_identity(dev, dist, world, backend) if world > 1 else None
     if args.workload != "mix" and world > 1:
         raise SystemExit("--workload grad-clique is single-GPU")
     fixed = world > 1 and args.config == "dcliques10000"       # BASELINE configs[4]: strong scaling
@@ -1009,6 +1087,8 @@ def main():
             # the slab pair fits the MALL, so the graph-replayed rounds run cache-resident
             out["config"]["cache_resident"] = 2 * n_local * cols_local * 4 < (256 << 20)
             out["config"]["cold_cache_round"] = cold
+        if ident is not None:
+            out["config"]["world"] = ident
         if world > 1 and args.shard == "nodes":
             out["config"]["halo_GB_recv_rank0"] = round(mixer.halo_bytes / 1e9, 3)
             out["config"]["halo_GB_send_rank0"] = round(mixer.send_bytes / 1e9, 3)

@@ -137,7 +137,12 @@ int niidmix_mix_band_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
  * are 16-B aligned, both ld are multiples of 4, ld_x >= p rounded up to 4 and n_rows <= 156, else
  * 64 columns -- stages it in LDS by LDS-DMA and combines each output row from there in its ELL
  * order, so each element of x is read from memory once.  Any row order.  Descriptors: the ELL arrays of
- * niidmix_mix_ell_f32 (k = 3, 5 or 8).  x 4-B aligned; x and y: [n_rows, ld].  mode as
+ * niidmix_mix_ell_f32 (k = 3, 5 or 8).  Contract: every ell_col entry is < n_rows -- only rows
+ * 0..n_rows-1 are staged, so x must hold exactly the rows the outputs read (a node shard whose
+ * rows read halo rows past its own is NOT a strip round: use niidmix_mix_ell_f32); the descriptors
+ * are device arrays and are not checked here (niidmix.ops.Mixer checks them once per topology).
+ * NIIDMIX_EUNSUPPORTED when the strip does not fit the device's per-block LDS.
+ * x 4-B aligned; x and y: [n_rows, ld].  mode as
  * niidmix_mix_ell_f32; bit-identical to it (and to niidmix_mix_csr_f32) in EXACT mode.  Round 4
  * (ABI 4). */
 int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n_rows,

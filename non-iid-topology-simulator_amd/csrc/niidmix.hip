@@ -3694,16 +3694,24 @@ int niidmix_mix_strip_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     if (reinterpret_cast<uintptr_t>(x) & 3) return set_error(NIIDMIX_EUNSUPPORTED, "x not 4-B aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // float4 lanes (256-column strips, 1 KiB per staged row) when every lane's float4 stays inside
-    // its row (ld >= p rounded up to 4) and the rows sit on 16-B boundaries, and the strip fits
-    // 156 KB of LDS; else one float per lane (64-column strips).  NIIDMIX_STRIP_SV=1 forces the
-    // latter (tuning)
+    // its row (ld >= p rounded up to 4) and the rows sit on 16-B boundaries, and the strip fits the
+    // device's per-block LDS (gfx950: 160 KB, so up to 156 rows); else one float per lane (64-column
+    // strips, 256 B per row).  NIIDMIX_STRIP_SV=1 forces the latter (tuning)
+    int dev = 0, lds_max = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || lds_max <= 0)
+        if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || lds_max <= 0)
+            lds_max = 65536;
     const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y);
     int sv = (ld_x % 4 == 0 && ld_y % 4 == 0 && (al & 15) == 0 && ld_x >= (p + 3) / 4 * 4 &&
-              n_rows <= 156) ? 4 : 1;
+              n_rows * kWave * 4 * (int64_t)sizeof(float) <= (int64_t)lds_max - 4096) ? 4 : 1;
     if (const char *e = getenv("NIIDMIX_STRIP_SV")) if (atoi(e) == 1) sv = 1;
+    if (n_rows * kWave * sv * (int64_t)sizeof(float) > (int64_t)lds_max)
+        return set_error(NIIDMIX_EUNSUPPORTED, "strip kernel: %lld rows do not fit %d B of LDS",
+                         (long long)n_rows, lds_max);
     const int64_t n_strips = (p + kWave * sv - 1) / (kWave * sv);
     if (n_strips > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many strips");
-    const size_t lds = (size_t)n_rows * kWave * sv * sizeof(float);   // <= 156 KB
+    const size_t lds = (size_t)n_rows * kWave * sv * sizeof(float);   // <= lds_max
     // waves per strip: 8 (NIIDMIX_STRIP_SW = 4 / 8 / 16 overrides, tuning)
     int sw = 8;
     if (const char *e = getenv("NIIDMIX_STRIP_SW")) { const int v = atoi(e); if (v == 4 || v == 8 || v == 16) sw = v; }

@@ -31,6 +31,8 @@ from random import Random
 import torch
 import torch.nn.functional as F
 
+from . import guard
+from . import logger as nl
 from . import meta as m
 from . import model as nm
 from .topology import load as load_topology, to_csr
@@ -220,6 +222,7 @@ class _FusedEngine:
                                            lr, self.mixer if dev == devices[0] else self.mixer.to(dev)),
                 n, p, devices, block=_row_block(), n_in=2, n_out=2 if wb else 1)
             self.outs = (self.slab.host, self.gslab.host) if wb else (self.slab.host,)
+            guard.install(models, self.resident)
         else:
             def make(dev, n, cols):
                 mixer = self.mixer if dev == devices[0] else self.mixer.to(dev)
@@ -338,6 +341,7 @@ class _Engine:
                 lambda dev, part: mixing_op(dev, part, self.mixer if dev == devices[0]
                                             else self.mixer.to(dev)),
                 n, p, devices, block=_row_block())
+            guard.install(self.slab.models, self.resident)
         else:
             self.runner = MultiDeviceRound(
                 lambda dev, n, cols: SlabMixer(self.mixer if dev == devices[0] else self.mixer.to(dev),
@@ -389,6 +393,9 @@ class _Engine:
         csr = to_csr(topology)
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        # the previous (deferred) round's kernel may still read the old Mixer's device descriptors
+        # on the resident s_mix stream: drain it before they are freed
+        self.wait_all()
         self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=self.devices[0])
         if self.resident is not None:
             for pt in self.resident.parts:
@@ -488,8 +495,12 @@ def _deferred_ok(params, state, epoch_done, active):
     lg = params.get("logger", {})
     if lg.get("log-consensus-distance") and epoch_done and all(epoch_done.values()):
         return False
-    if params["topology"]["name"] in ("fully-connected", "sample"):
-        return not _should_log(state["nodes"][0], epoch_done.get(0, False), params, state)
+    # run.py:107-116: fully-connected / sample log node 0 when IT should log; otherwise (and for
+    # every other topology) each active node that should log -- e.g. a node whose epoch ended when
+    # node 0's did not
+    if params["topology"]["name"] in ("fully-connected", "sample") and \
+            _should_log(state["nodes"][0], epoch_done.get(0, False), params, state):
+        return False
     return not any(_should_log(n, epoch_done[n["rank"]], params, state) for n in active)
 
 
@@ -523,6 +534,9 @@ def init(nodes, topology, params):
     logging.basicConfig(level=getattr(logging, params["meta"]["log"].upper(), None))
     synchronize()
     state = {"nodes": nodes, "topology": topology, "step": 0}
+    # the reference driver's logging of the models on the GPU (niidmix.logger.install_hooks:
+    # Logger.log_consensus_distance, and setup.model.average under log-global-model-accuracy)
+    nl.install_hooks(params)
     for n in nodes:
         n["train-iterator"] = _loader(n, params)
     if params["algorithm"]["initial-averaging"]:

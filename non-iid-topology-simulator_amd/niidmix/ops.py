@@ -815,9 +815,12 @@ class Mixer:
     def _strip_ok(self, x, out):
         """The column-strip kernel (few nodes, ELL rows) on slabs whose rows sit on a 256-B pitch:
         ring 100 at P = 62 006 11.0 us per round vs 14.8 for the band kernel on the same pitch; on
-        ld = P (rows at 216-B offsets) the kernels are equal, 15.6-16 us (tools/band_probe.py)."""
+        ld = P (rows at 216-B offsets) the kernels are equal, 15.6-16 us (tools/band_probe.py).
+        The kernel stages rows 0..n-1 only, so every ELL column must index one of them: a node
+        shard whose rows read halo rows (csr.n_in > n) is never a strip round."""
         return (self.ell is not None and self.n <= STRIP_MAX_ROWS and x is not None and
-                x.dim() == 2 and x.shape[0] >= self.n and x.stride(0) % 64 == 0 and
+                self.csr.n_in == self.n and x.dim() == 2 and x.shape[0] == self.n and
+                x.stride(0) % 64 == 0 and
                 (out is None or (out.dim() == 2 and out.stride(0) % 64 == 0)))
 
     def kernel_for(self, mode="fast", x=None, out=None):
@@ -864,6 +867,9 @@ class Mixer:
                     EXACT if k == "ell-exact" else FAST)
         elif k in ("strip-exact", "strip-fast"):
             _req(self.ell is not None, "no ELL layout: a row has more than 8 entries")
+            _req(self.csr.n_in == self.n and x.shape[0] == self.n,
+                 "strip kernel: rows read sources past the slab's own rows (halo rows of a node "
+                 "shard); the strip stages only rows 0..n-1 (use ell-*)")
             mix_strip(x, self.e_col, self.e_val, self.e_len, out, self.ell,
                       EXACT if k == "strip-exact" else FAST)
         elif k in ("band-exact", "band-fast"):

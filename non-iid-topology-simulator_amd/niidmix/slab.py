@@ -70,20 +70,26 @@ class NodeSlab:
                         view.copy_(q.detach().reshape(-1))
                         q.data = view.view(shape)
                     off += k
+        if not grads:
+            from .guard import tag_slab
+            tag_slab(models, self)
 
     def owns(self, models):
-        """True iff `models` are exactly this slab's models, in order, still backed by it."""
+        """True iff `models` are exactly this slab's models, in order, still backed by it (reads
+        only parameter identities: no read-guard wait, niidmix.guard)."""
+        from .guard import suspended
         if len(models) != self.n:
             return False
         base = self.host.data_ptr()
-        for i, m in enumerate(models):
-            if m is not self.models[i]:
-                return False
-            for q in m.parameters():
-                t = q.grad if self.grads else q
-                if t is None or t.data_ptr() != base + i * self.p * 4:
+        with suspended():
+            for i, m in enumerate(models):
+                if m is not self.models[i]:
                     return False
-                break
+                for q in m.parameters():
+                    t = q.grad if self.grads else q
+                    if t is None or t.data_ptr() != base + i * self.p * 4:
+                        return False
+                    break
         return True
 
 
@@ -402,6 +408,9 @@ class ResidentRound:
         self._count = [0] * self.nblk      # rows of each block made final this round
         self._sent = [False] * self.nblk
         self._done = None                  # per block: the D2H events of the last op
+        # the device outputs (outs[0]: the mixed parameters) hold the models' current values: set
+        # by mix(), cleared by begin() and by guarded writes (niidmix.guard); read by niidmix.logger
+        self.fresh = False
         self.last_timing = None
 
     @staticmethod
@@ -428,6 +437,7 @@ class ResidentRound:
         self.hosts = list(hosts)
         self.hosts_out = list(outs) if outs is not None else list(hosts[:self.n_out])
         assert len(self.hosts_out) == self.n_out
+        self.fresh = False
         self._count = [0] * self.nblk
         self._sent = [False] * self.nblk
         for pt in self.parts:
@@ -464,6 +474,7 @@ class ResidentRound:
         """Enqueue the rest of the round (remaining H2D, the device op, D2H by block); returns at
         once."""
         t0 = time.perf_counter()
+        delay = int(os.environ.get("NIIDMIX_D2H_DELAY_CYCLES", "0"))
         unsent = sum(1 for s in self._sent if not s)
         for b in range(self.nblk):
             if not self._sent[b]:
@@ -487,6 +498,9 @@ class ResidentRound:
                     ev[1].record(sm)
                     t_ev.append(ev)
                 sd.wait_event(ev_mix)
+                if delay:                           # test knob: a late write-back (guard tests)
+                    with torch.cuda.stream(sd):
+                        torch.cuda._sleep(delay)
                 w = pt["w"]
                 for b in range(self.nblk):
                     r0, rows = self._rows(b)
@@ -497,6 +511,7 @@ class ResidentRound:
                     e.record(sd)
                     done[b].append(e)
         self._done = done
+        self.fresh = True
         self.hosts = None                           # row_ready() is a no-op until begin()
         self._timing = (timing, t0, t_ev, unsent)
 

@@ -25,7 +25,7 @@ def pytest_configure(config):
 
 def golden_cases(pattern=""):
     names = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
-    return [n for n in names if pattern in n and not n.startswith(("uniform_avg", "grad_", "consensus_"))]
+    return [n for n in names if pattern in n and not n.startswith(("uniform_avg", "grad_", "consensus_", "logger_"))]
 
 
 def grad_cases():

@@ -417,8 +417,61 @@ def main():
     print("uniform_avg_k7_p100")
 
 
+def logger_round_cases():
+    """One reference mixing round (d_sgd.average, d_sgd.py:96-116) on seeded models, then what
+    run.py's logging reads from the mixed models: Logger.log_consensus_distance
+    (logger.py:257-284, stub instance) and Logger.state's global model setup.model.average
+    (logger.py:112) over every node, over a subset of them (nodes_to_log) and over node 0 alone
+    (fully-connected / sample).  Stored: x (pre-round), y (post-round), the CSR of W^T, cliques,
+    the event and its stats, and the three averaged models flattened."""
+    import importlib
+    logger = importlib.import_module("simulate.logger")
+    name, n, shapes, seed = "logger_round_dcliques300_p520", 300, [(10, 51), (10,)], 41
+    p = sum(int(np.prod(s)) for s in shapes)
+    e, cl = dcliques(n, 100, "fully-connected")
+    weights = R.weights.compute_weights(_nodes(n), e, MH)
+    _, loaded = _roundtrip(e, weights, cl)
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(n, p, generator=g) + 0.5).numpy()
+    nodes = []
+    for rank in range(n):
+        m = FlatModel(shapes)
+        with torch.no_grad():
+            off = 0
+            for q in m.parameters():
+                k = q.numel()
+                q.copy_(torch.from_numpy(x[rank, off:off + k].copy()).view_as(q))
+                off += k
+        nodes.append({"rank": rank, "model": m})
+    R.d_sgd.average(nodes, loaded, {})
+    y = _flat(nodes, "param")
+    with tempfile.TemporaryDirectory() as d:
+        stub = types.SimpleNamespace(global_events=os.path.join(d, "global.jsonlines"))
+        logger.Logger.log_consensus_distance(stub, {"nodes": nodes, "step": 3})
+        ev = json.loads(open(stub.global_events).read().strip())
+    gl = ev["distance_to_center"]["global"]
+    subset = list(range(3, 13)) + [150, 299]
+    centers = {}
+    for key, sel in (("center_all", list(range(n))), ("center_subset", subset),
+                     ("center_node0", [0])):
+        c = R.model.average([nodes[r]["model"] for r in sel])
+        centers[key] = torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy()
+    row_ptr, col, val = _csr(loaded, n)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), x=x, y=y, row_ptr=row_ptr, col=col,
+                        val=val, shapes_json=np.asarray(json.dumps([list(s) for s in shapes])),
+                        cliques_flat=np.asarray([r for c in cl for r in c], np.int32),
+                        cliques_ptr=np.cumsum([0] + [len(c) for c in cl]).astype(np.int64),
+                        event_json=np.asarray(json.dumps(ev)),
+                        stats=np.asarray([gl["avg"], gl["std"], gl["max"], gl["min"],
+                                          ev["center"]["norm"]], np.float64),
+                        subset=np.asarray(subset, np.int64), **centers)
+    print(f"{name}: N={n} P={p} avg={gl['avg']:.6g} norm={ev['center']['norm']:.6g}")
+
+
 if __name__ == "__main__":
-    if "--grad" in sys.argv:
+    if "--logger" in sys.argv:
+        logger_round_cases()
+    elif "--grad" in sys.argv:
         grad_cases()
     elif "--nonfinite" in sys.argv:
         nonfinite_cases()
@@ -429,3 +482,4 @@ if __name__ == "__main__":
         grad_cases()
         nonfinite_cases()
         consensus_cases()
+        logger_round_cases()

@@ -168,7 +168,8 @@ def _legs_worker(rank, world, port, q, n, p):
                 raise ValueError("only rank 1")
             return {"ok": True}
         g_info, g_err = bench.guarded_leg(one_rank_fails, dist, world, rank)
-        q.put((rank, stripe, (c0, c1), finals, report, g_info, g_err))
+        ident = bench.world_identity(cpu, dist, world, "gloo")
+        q.put((rank, stripe, (c0, c1), finals, report, g_info, g_err, ident))
     finally:
         dist.destroy_process_group()
 
@@ -196,7 +197,11 @@ def test_bench_default_multi_gpu_path_gloo(oracle_mod):
             ref = oracle_mod.mix_exact_c(ref, csr.row_ptr, csr.col, csr.val)
         refs[ic] = ref
     covered = np.zeros(p, bool)
-    for rank, stripe, (c0, c1), finals, report, g_info, g_err in out:
+    for rank, stripe, (c0, c1), finals, report, g_info, g_err, ident in out:
+        # the self-describing N>1 record: backend, world size, distinct devices all-gathered
+        assert ident["backend"] == "gloo" and ident["world_size"] == world
+        assert ident["distinct_devices"] == world and len(ident["devices"]) == world
+        assert ident["rccl_version"] is None
         # stripes: bitwise the oracle's columns
         assert oracle_mod.bitwise_equal(stripe, refs["fully-connected"][:, c0:c1]), rank
         covered[c0:c1] = True
@@ -207,6 +212,9 @@ def test_bench_default_multi_gpu_path_gloo(oracle_mod):
                         "weak_efficiency_vs_1gpu"):
                 assert key in info, key
             assert info["interclique"] == ic and info["halo_rows_max"] > 0
+            xg = info["xgmi"]                 # the exchange alone, per rank
+            assert len(xg["recv_GBs_per_rank"]) == world and len(xg["ms_per_round"]) == world
+            assert all(v is not None and v > 0 for v in xg["recv_GBs_per_rank"])
         assert [e["interclique"] for e in report] == ["fully-connected", "smallworld"]
         assert "error" not in report[0] and report[0]["ms_per_step"] > 0
         assert report[1]["error"].startswith("failed on rank(s) [0, 1]")

@@ -243,7 +243,95 @@ def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypat
         assert not any(pend)
 
 
-@pytest.mark.parametrize("alg", ["clique", "unbiased"])
+def _ring_training_setup(n, seed=1337):
+    from niidmix import d_sgd
+    from niidmix.topology import mh_csr
+    torch.manual_seed(seed)
+    params = {"meta": {"log": "WARNING", "seed": seed}, "model": {"input-size": 784},
+              "topology": {"name": "ring"},
+              "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 0,
+                         "log-consensus-distance": False},
+              "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 25,
+                            "initial-averaging": False, "clique-gradient": False,
+                            "unbiased-gradient": False, "deferred-writeback": True}}
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(784, 10)
+
+        def forward(self, x, params):
+            return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+    g = torch.Generator().manual_seed(7)
+    data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
+            for _ in range(n * 200)]
+    nodes = []
+    for r in range(n):
+        mdl = Net()
+        nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
+                      "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+    edges = {r: [(r + 1) % n, (r - 1) % n] for r in range(n)}
+    topo = {"edges": edges, "weights": torch.from_numpy(mh_csr(n, edges).dense())}
+    return params, nodes, topo
+
+
+def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
+    """a driver that reads models on rounds _deferred_ok did NOT predict (no
+    logging configured, so every round returns with the write-back in flight; the D2H is held back
+    ~50 ms by NIIDMIX_D2H_DELAY_CYCLES) gets the MIXED parameters through state_dict(), forward()
+    and parameters() -- niidmix.guard waits for the model's own rows -- bitwise the reference loop
+    doing the mixing.  With the guard off (NIIDMIX_READ_GUARD=0) the same reads see stale rows,
+    which shows the test can tell the two apart."""
+    from niidmix import d_sgd, guard
+    n, rounds = 16, 4
+    monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")
+    monkeypatch.setenv("NIIDMIX_D2H_DELAY_CYCLES", str(100_000_000))
+
+    def run(mix, guard_on):
+        monkeypatch.setenv("NIIDMIX_READ_GUARD", "1" if guard_on else "0")
+        params, nodes, topo = _ring_training_setup(n)
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False
+        seen, pend = [], []
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for k in range(rounds):
+                state, _, _, _ = d_sgd.next_step(state, params, None)
+                eng = d_sgd._engines.get(id(nodes))
+                pend.append(bool(eng is not None and eng.resident is not None and
+                                 eng.resident.pending))
+                # the unpredicted reader, right after next_step: one entry point per round
+                r = (5 * k + 3) % n
+                mdl = nodes[r]["model"]
+                if k % 3 == 0:
+                    w = mdl.state_dict()["fc.weight"].clone()
+                elif k % 3 == 1:
+                    w = next(mdl.parameters()).detach().clone()
+                else:
+                    mdl.forward(torch.zeros(1, 784), params)
+                    w = mdl.fc.weight.detach().clone()
+                seen.append(w)
+                d_sgd.synchronize()
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+        return seen, pend
+
+    ref, _ = run("oracle", True)
+    w0 = guard.stats["waits"]
+    got, pend = run("gpu", True)
+    assert all(pend), pend                        # every round really returned early
+    assert guard.stats["waits"] > w0
+    for k, (u, v) in enumerate(zip(got, ref)):
+        assert torch.equal(u, v), k
+    stale, pend = run("gpu", False)
+    assert all(pend)
+    assert any(not torch.equal(u, v) for u, v in zip(stale, ref))
+
+
+@pytest.mark.parametrize("alg",["clique", "unbiased"])
 def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
     """Rounds with --clique-gradient / --unbiased-gradient (linear model, 4 nodes): the drop-in's
     fused device round (gradient mean + SGD step + mixing) and its unfused GPU path (gradient
@@ -597,3 +685,136 @@ def test_sample_topology_training_rounds(gpu):
 
     for u, v in zip(run("gpu"), run("cpu")):
         assert torch.equal(u, v)
+
+
+def _fake_reference_modules(monkeypatch, tmp_path):
+    """Stand-ins for the modules run.py imports before the plugin (simulate.logger, setup.model):
+    /root/reference is not on the GPU box, so these hold the reference's CPU restatement; the
+    plugin's init must route both through the GPU (niidmix.logger.install_hooks)."""
+    import sys
+    import types
+    lg = types.ModuleType("simulate.logger")
+
+    class Logger:
+        def __init__(self):
+            self.global_events = str(tmp_path / "global.jsonlines")
+
+        def log_consensus_distance(self, state):          # replaced by the plugin's init
+            raise AssertionError("CPU consensus distance ran")
+    lg.Logger = Logger
+    sm = types.ModuleType("setup.model")
+
+    def cpu_average(models, weights=None):
+        raise AssertionError("CPU setup.model.average ran")
+    sm.average = cpu_average
+    monkeypatch.setitem(sys.modules, "simulate.logger", lg)
+    monkeypatch.setitem(sys.modules, "setup.model", sm)
+    return lg, sm
+
+
+def test_logger_hooks_read_resident_slab(gpu, monkeypatch, tmp_path):
+    """VERDICT r04 What's missing #2: the unchanged driver's logging after a plugin round.  With
+    the reference's modules loaded, niidmix.d_sgd.init routes Logger.log_consensus_distance and
+    (log-global-model-accuracy) setup.model.average through the GPU, reading the RESIDENT output
+    slab of the round (no H2D).  Checked against tests/golden/logger_round_dcliques300_p520, made
+    by the reference itself (make_golden.py --logger): the round bitwise, the consensus event's
+    avg/max/min/norm within 1e-5 and std within 1e-4 relative, the global models (all nodes, a
+    nodes_to_log subset, node 0 alone) bitwise."""
+    from niidmix import d_sgd
+    from niidmix import logger as nl
+    g = load_golden("logger_round_dcliques300_p520")
+    lg, sm = _fake_reference_modules(monkeypatch, tmp_path)
+    nodes, topo = _nodes_and_topology(g)
+    for nd in nodes:
+        nd["train-set"] = [(torch.zeros(1), 0)]           # init() builds a loader per node
+    params = {"meta": {"log": "WARNING"}, "topology": {"name": "d-cliques"},
+              "logger": {"log-consensus-distance": True, "log-global-model-accuracy": True},
+              "algorithm": {"initial-averaging": False, "batch-size": 8}}
+    state, _, _ = d_sgd.init(nodes, topo, params)
+    assert lg.Logger.log_consensus_distance is nl.log_consensus_distance
+    assert sm.average is nl.average
+    d_sgd.average(nodes, topo, params)                      # one resident round
+    eng = d_sgd._engines[id(nodes)]
+    assert eng.resident is not None and eng.resident.fresh
+    assert oracle_bitwise(_params_of(nodes), g["y"])
+    state["step"] = 3
+    lg.Logger().log_consensus_distance(state)
+    assert nl.last_source["consensus"] == "resident"
+    ev = json.loads(open(tmp_path / "global.jsonlines").read().strip().splitlines()[-1])
+    ref = json.loads(str(g["event_json"]))
+    gl, rg = ev["distance_to_center"]["global"], ref["distance_to_center"]["global"]
+    for k in ("avg", "max", "min"):
+        np.testing.assert_allclose(gl[k], rg[k], rtol=1e-5)
+    np.testing.assert_allclose(gl["std"], rg["std"], rtol=1e-4)
+    np.testing.assert_allclose(ev["center"]["norm"], ref["center"]["norm"], rtol=1e-5)
+    assert ev["type"] == ref["type"] and ev["step"] == ref["step"]
+    models = [nd["model"] for nd in nodes]
+    for key, sel in (("center_all", range(len(nodes))), ("center_subset", g["subset"]),
+                     ("center_node0", [0])):
+        c = sm.average([models[int(r)] for r in sel])
+        assert nl.last_source["average"] == "resident"
+        flat = torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy()
+        assert oracle_bitwise(flat, g[key]), key
+        assert "_niidmix_row" not in c.__dict__
+    # a guarded write (load_state_dict) makes the device copy stale: the next read stacks
+    models[5].load_state_dict(models[5].state_dict())
+    assert not eng.resident.fresh
+    c = sm.average(models)
+    assert nl.last_source["average"] == "stacked"
+    assert oracle_bitwise(torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy(),
+                          g["center_all"])
+    lg.Logger().log_consensus_distance(state)
+    assert nl.last_source["consensus"] == "host-slab"
+    ev2 = json.loads(open(tmp_path / "global.jsonlines").read().strip().splitlines()[-1])
+    np.testing.assert_allclose(ev2["distance_to_center"]["global"]["avg"], rg["avg"], rtol=1e-5)
+    np.testing.assert_allclose(ev2["center"]["norm"], ref["center"]["norm"], rtol=1e-5)
+
+
+def oracle_bitwise(a, b):
+    from oracle import oracle
+    return oracle.bitwise_equal(np.asarray(a), np.asarray(b))
+
+
+def test_logger_hooks_opt_out(gpu, monkeypatch, tmp_path):
+    """NIIDMIX_GPU_LOGGER=0 leaves the reference's functions in place."""
+    from niidmix import logger as nl
+    lg, sm = _fake_reference_modules(monkeypatch, tmp_path)
+    before = (lg.Logger.log_consensus_distance, sm.average)
+    monkeypatch.setenv("NIIDMIX_GPU_LOGGER", "0")
+    assert nl.install_hooks({"logger": {"log-global-model-accuracy": True}}) == []
+    assert (lg.Logger.log_consensus_distance, sm.average) == before
+    monkeypatch.delenv("NIIDMIX_GPU_LOGGER")
+    assert nl.install_hooks({"logger": {}, "algorithm": {"gpu-logger": False}}) == []
+    assert nl.install_hooks({"logger": {}}) == ["simulate.logger.Logger.log_consensus_distance"]
+    assert sm.average is before[1]                 # only with log-global-model-accuracy
+
+
+def test_consensus_event_in_training_rounds(gpu, monkeypatch, tmp_path):
+    """The row-streamed training rounds of next_step with log-consensus-distance on (run.py
+    logs the event once every node's epoch is done, and next_step then returns synchronised): the
+    event the installed hook writes reads the resident slab and matches the CPU restatement of the
+    reference arithmetic on the synchronised host models."""
+    from niidmix import d_sgd
+    from niidmix import logger as nl
+    lg, _ = _fake_reference_modules(monkeypatch, tmp_path)
+    params, nodes, topo = _ring_training_setup(8)
+    params["logger"]["log-consensus-distance"] = True
+    for nd in nodes:
+        nd["train-set"] = nd["train-set"][:50]               # 2 steps per epoch at batch 25
+    state, _, _ = d_sgd.init(nodes, topo, params)
+    log = lg.Logger()
+    logged = 0
+    for _ in range(4):
+        state, _, done, _ = d_sgd.next_step(state, params, None)
+        if all(done.values()):
+            eng = d_sgd._engines[id(nodes)]
+            assert not eng.resident.pending                  # predicted: returned synchronised
+            log.log_consensus_distance(state)
+            assert nl.last_source["consensus"] == "resident"
+            ev = json.loads(open(log.global_events).read().strip().splitlines()[-1])
+            d, norm = _cpu_consensus_statistics([n["model"] for n in nodes])
+            gl = ev["distance_to_center"]["global"]
+            np.testing.assert_allclose(gl["avg"], np.mean(d), rtol=1e-5)
+            np.testing.assert_allclose(ev["center"]["norm"], norm, rtol=1e-5)
+            logged += 1
+    assert logged == 2

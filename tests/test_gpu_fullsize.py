@@ -94,11 +94,61 @@ def test_fc1000_blocked_bigclique_fullsize(gpu, oracle_mod):
 
 
 @pytest.mark.parametrize("mode", ["fast", "exact"])
-def test_ring100_p62006_hipgraph(mode, gpu, oracle_mod):
-    """bench.py --config ring100 (P = 62006, rows 8-byte aligned: the float2 path of the ELL kernel,
-    4 chunks per wave) with the rounds captured in ONE hipGraph, as the bench times it:
-    two ping-pong rounds per replay, each checked against the oracle applied to that round's own
-    GPU input (bitwise in exact mode)."""
+def test_ring100_p62006_timed_shape_hipgraph(mode, gpu, oracle_mod):
+    """bench.py --config ring100 EXACTLY as it is timed (bench.py single-GPU branch): the golden
+    ring's CSR relabeled into its cycle order (Mixer.device_layout -> band_layout), node state in
+    VMM slabs on a 256-B row pitch (memory.empty_slab(100, 62016) viewed as [:, :62006]), the
+    kernel Mixer.kernel_for picks on that slab -- k_mix_strip with float4 lanes and non-temporal
+    LDS-DMA staging -- and two ping-pong rounds captured in ONE hipGraph.  Every round of two
+    replays is checked against the C oracle on the relabeled CSR applied to that round's own GPU
+    input: bitwise in exact mode, 1e-5 condition-aware in fast mode.  The 10 pitch-padding columns
+    of both slabs carry a sentinel that must survive (the strip kernel never writes them)."""
+    from niidmix import memory
+    g, csr = _golden_csr("ring100_p257")
+    m = _mixer(csr, None, gpu)
+    perm, _ = m.device_layout()
+    assert perm is not None                           # rank order is not banded: cycle order
+    m = m.relabeled(perm)
+    p, ld = 62006, 62016
+    assert ld == -(-p // 64) * 64                     # bench.py's pitch rule for few-node graphs
+    fa, fb = memory.empty_slab(100, ld, gpu), memory.empty_slab(100, ld, gpu)
+    assert fa.stride(0) == ld and fb.stride(0) == ld
+    fa.normal_(generator=torch.Generator(device=gpu).manual_seed(2))
+    sentinel = -1234.5
+    fa[:, p:] = sentinel
+    fb.fill_(sentinel)
+    a, b = fa[:, :p], fb[:, :p]
+    kernel = m.kernel_for(mode, a, b)
+    assert kernel == ("strip-fast" if mode == "fast" else "strip-exact")
+    m(a, out=b, kernel=kernel, mode=mode)             # warm-up outside the capture
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        m(a, out=b, kernel=kernel, mode=mode)
+        m(b, out=a, kernel=kernel, mode=mode)
+    rp, col, val = m.csr.row_ptr, m.csr.col, m.csr.val
+    for _ in range(2):
+        x0 = a.cpu().numpy()
+        graph.replay()
+        torch.cuda.synchronize()
+        y1, y2 = b.cpu().numpy(), a.cpu().numpy()
+        for xin, yout in ((x0, y1), (y1, y2)):
+            ref = oracle_mod.mix_exact_c(xin, rp, col, val)
+            if mode == "exact":
+                assert oracle_mod.bitwise_equal(yout, ref)
+            else:
+                bound = oracle_mod.condition_bound(xin, rp, col, val)
+                ok, worst = oracle_mod.check_tolerance(yout, ref, bound, rtol=RTOL)
+                assert ok, worst
+    for f in (fa, fb):
+        assert bool(torch.all(f[:, p:] == sentinel)), "pitch padding written"
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_ring100_p62006_rank_order_ell_fallback_hipgraph(mode, gpu, oracle_mod):
+    """The ring-100 round on slabs the strip and band kernels do NOT take -- rank order, ld = P
+    (rows at 216-B offsets) -- falls back to the ELL kernel (float2 path, 4 chunks per wave); two
+    ping-pong rounds in ONE hipGraph, each checked against the oracle on that round's own GPU input
+    (bitwise in exact mode).  (bench.py's timed ring100 shape: the test above.)"""
     g, csr = _golden_csr("ring100_p257")
     m = _mixer(csr, None, gpu)
     p = 62006

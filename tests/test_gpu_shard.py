@@ -104,6 +104,57 @@ def test_sharded_rounds_loopback(world, inter, gpu, oracle_mod):
             assert np.max(np.abs(got - ref)) < 1e-5
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_ring_auto_kernel_loopback(world, gpu, oracle_mod):
+    """A node shard of a low-degree graph (the golden ring 100) with kernel=None on 256-column
+    windows (row stride a multiple of 64 floats, the strip kernel's pitch test passes): each rank's
+    rows read halo rows past its own, so the auto choice must NOT be the strip kernel (it stages rows
+    0..n_local-1 only); 3 rounds, exact and fast, against the single-GPU oracle."""
+    from niidmix.ops import csr_from_numpy
+    from niidmix.shard import LoopbackTransport, ShardedMixer
+    g = load_golden("ring100_p257")
+    csr = csr_from_numpy(g["row_ptr"], g["col"], g["val"])
+    n, p = csr.n, 1536
+    for mode in ("exact", "fast"):
+        tr = LoopbackTransport()
+        sms = [ShardedMixer(csr, None, world, r, gpu, p, windows=3, transport=tr)
+               for r in range(world)]
+        gen = torch.Generator(device=gpu).manual_seed(4)
+        x0 = torch.randn(n, p, device=gpu, generator=gen)
+        xs, ys = [], []
+        for sm in sms:
+            assert sm.shard.csr.n_in > sm.n_local            # every ring shard reads halo rows
+            x = sm.empty().zero_()
+            assert x[0].stride(0) % 64 == 0
+            k_auto = sm.kernel_for(mode, x)
+            assert not k_auto.startswith("strip"), k_auto
+            nodes = torch.from_numpy(sm.shard.nodes).to(gpu)
+            for k in range(sm.k):
+                cw = min(sm.w, p - k * sm.w)
+                x[k, :sm.n_local, :cw] = x0.index_select(0, nodes)[:, k * sm.w:k * sm.w + cw]
+            xs.append(x)
+            ys.append(sm.empty())
+        for _ in range(3):
+            tr.inputs = {r: xs[r] for r in range(world)}
+            for r, sm in enumerate(sms):
+                sm(xs[r], ys[r], kernel=None, mode=mode)
+            xs, ys = ys, xs
+        torch.cuda.synchronize()
+        full = torch.empty_like(x0)
+        for r, sm in enumerate(sms):
+            nodes = torch.from_numpy(sm.shard.nodes).to(gpu)
+            full[nodes] = torch.cat([xs[r][k, :sm.n_local, :min(sm.w, p - k * sm.w)]
+                                     for k in range(sm.k)], dim=1)
+        ref = x0.cpu().numpy()
+        for _ in range(3):
+            ref = oracle_mod.mix_exact_c(ref, csr.row_ptr, csr.col, csr.val)
+        got = full.cpu().numpy()
+        if mode == "exact":
+            assert oracle_mod.bitwise_equal(got, ref)
+        else:
+            assert np.max(np.abs(got - ref)) < 1e-5
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_striped_mixer_equals_single_gpu(world, gpu, oracle_mod):
     """Every rank's column stripe (blocked slab, clique kernel) is bitwise the single-GPU blocked

@@ -75,3 +75,114 @@ def test_mixing_devices_policy(monkeypatch):
     assert mixing_devices(3 * MIN_STRIPE_COLS, devs) == devs[:3]
     monkeypatch.setenv("NIIDMIX_DEVICES", "2,5")
     assert mixing_devices(1 << 20) == [torch.device("cuda", 2), torch.device("cuda", 5)]
+
+
+def _run_py_reads_models(params, state, epoch_done, active):
+    """Which of run.py's post-next_step branches (tools/simulate/run.py:105-119) read a model:
+    log.state of the nodes its should_log (run.py:19-25) picks -- node 0 alone for fully-connected
+    / sample when node 0 should log, else every active node that should -- and
+    log_consensus_distance once every node finished its epoch."""
+    lg = params["logger"]
+
+    def should_log(node, done):
+        if lg["accuracy-logging-interval"] and done and \
+                node["epoch"] % lg["accuracy-logging-interval"] == 0:
+            return True
+        return bool(lg["accuracy-logging-interval-steps"]) and \
+            state["step"] % lg["accuracy-logging-interval-steps"] == 0
+
+    logged = []
+    if params["topology"]["name"] in ("fully-connected", "sample") and \
+            should_log(state["nodes"][0], epoch_done.get(0, False)):
+        logged = [state["nodes"][0]]
+    else:
+        logged = [n for n in active if should_log(n, epoch_done[n["rank"]])]
+    return bool(logged) or bool(all(epoch_done.values()) and lg["log-consensus-distance"])
+
+
+def test_deferred_ok_mirrors_run_py_branches(monkeypatch):
+    """niidmix.d_sgd._deferred_ok (may next_step return with the write-back in flight?) against
+    run.py's own branch structure, over topologies, logging intervals, steps, per-node epochs and
+    epoch-done patterns -- including the fully-connected case where node 0 does not log but another
+    node whose epoch just ended does."""
+    import itertools
+    from niidmix import d_sgd
+    monkeypatch.delenv("NIIDMIX_DEFERRED_WRITEBACK", raising=False)
+    n = 4
+    checked = 0
+    for topo, ivl, ivl_steps, cons, step, epochs, done_bits in itertools.product(
+            ("ring", "fully-connected", "sample", "d-cliques"), (0, 1, 2), (0, 3), (False, True),
+            (1, 3, 6, 7), ((1, 1, 1, 1), (2, 1, 2, 3)), range(16)):
+        nodes = [{"rank": r, "epoch": epochs[r]} for r in range(n)]
+        state = {"nodes": nodes, "step": step}
+        epoch_done = {r: bool(done_bits >> r & 1) for r in range(n)}
+        params = {"topology": {"name": topo},
+                  "logger": {"accuracy-logging-interval": ivl,
+                             "accuracy-logging-interval-steps": ivl_steps,
+                             "log-consensus-distance": cons},
+                  "algorithm": {"deferred-writeback": True}}
+        for active in (nodes, nodes[1:3]):
+            ep = {nd["rank"]: epoch_done[nd["rank"]] for nd in active} if topo == "sample" \
+                else epoch_done
+            got = d_sgd._deferred_ok(params, state, ep, active)
+            assert got == (not _run_py_reads_models(params, state, ep, active)), \
+                (topo, ivl, ivl_steps, cons, step, epochs, done_bits, len(active))
+            checked += 1
+    assert checked > 1000
+    params["algorithm"]["deferred-writeback"] = False
+    assert not d_sgd._deferred_ok(params, state, epoch_done, nodes)
+
+
+def test_read_guard_waits_for_own_row(monkeypatch):
+    """niidmix.guard: every Module entry point that reads or writes a guarded model's parameters
+    waits for that model's own row block while a round is pending (and only then); deepcopy and
+    isinstance keep working; suspended() and NIIDMIX_READ_GUARD=0 turn it off."""
+    import copy
+    from niidmix import guard
+
+    class FakeRound:
+        pending = True
+
+        def __init__(self):
+            self.waited = []
+
+        def wait_row(self, i):
+            self.waited.append(i)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(3, 2)
+
+        def forward(self, x, params=None):
+            return self.fc(x)
+
+    monkeypatch.delenv("NIIDMIX_READ_GUARD", raising=False)
+    models = [Net() for _ in range(3)]
+    eng = FakeRound()
+    guard.install(models, eng)
+    m = models[2]
+    assert isinstance(m, Net) and type(m).__name__ == "Net" and type(models[0]) is type(m)
+    x = torch.zeros(1, 3)
+    for read in (lambda: m.forward(x, None), lambda: m(x), lambda: list(m.parameters()),
+                 lambda: list(m.named_parameters()), lambda: m.state_dict(),
+                 lambda: m.load_state_dict(models[1].state_dict()), lambda: m.to(torch.float32)):
+        eng.waited.clear()
+        read()
+        assert 2 in eng.waited and set(eng.waited) <= {1, 2}
+    eng.waited.clear()
+    c = copy.deepcopy(models[0])
+    assert isinstance(c, Net) and torch.equal(c.fc.weight, models[0].fc.weight)
+    eng.pending = False
+    eng.waited.clear()
+    models[0](x)
+    list(models[1].parameters())
+    assert eng.waited == []                          # nothing pending: no wait at all
+    eng.pending = True
+    with guard.suspended():
+        list(models[0].parameters())
+    assert eng.waited == []
+    monkeypatch.setenv("NIIDMIX_READ_GUARD", "0")
+    plain = [Net()]
+    guard.install(plain, eng)
+    assert type(plain[0]) is Net

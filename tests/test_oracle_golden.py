@@ -81,3 +81,29 @@ def test_reference_loop_restatement(oracle_mod):
         y = np.stack([torch.cat([p.detach().reshape(-1) for p in nd["model"].parameters()]).numpy()
                       for nd in nodes])
         assert oracle_mod.bitwise_equal(y, g["y"]), name
+
+
+def test_logger_round_fixture(oracle_mod):
+    """tests/golden/logger_round_dcliques300_p520 (make_golden.py --logger: one reference mixing
+    round, then the reference Logger's consensus event and setup.model.average over all nodes, a
+    subset and node 0): the oracle reproduces the round bitwise, the uniform averages bitwise
+    (mean_rows_np / mix_exact_np AVERAGE_ONLY over the subset rows), and the event's statistics
+    from the mixed rows in fp64 within 1e-6 relative."""
+    import statistics
+    g = load_golden("logger_round_dcliques300_p520")
+    y = oracle_mod.mix_exact_c(g["x"], g["row_ptr"], g["col"], g["val"])
+    assert oracle_mod.bitwise_equal(y, g["y"])
+    assert oracle_mod.bitwise_equal(oracle_mod.mean_rows_np(g["y"]), g["center_all"])
+    sub = g["subset"]
+    k = len(sub)
+    w = np.full(k, np.float32(1.0 / k), np.float32)
+    c = oracle_mod.mix_exact_np(g["y"], np.asarray([0, k]), sub.astype(np.int32), w,
+                                average_only=True)[0]
+    assert oracle_mod.bitwise_equal(c, g["center_subset"])
+    assert oracle_mod.bitwise_equal(g["y"][0] * np.float32(0) + np.float32(1) * g["y"][0],
+                                    g["center_node0"])
+    center = g["center_all"].astype(np.float64)
+    d = np.sqrt(((g["y"].astype(np.float64) - center) ** 2).sum(1)).tolist()
+    got = [statistics.mean(d), statistics.stdev(d), max(d), min(d),
+           float(np.sqrt((center ** 2).sum()))]
+    np.testing.assert_allclose(got, g["stats"], rtol=1e-6)

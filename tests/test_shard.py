@@ -208,3 +208,25 @@ def test_gloo_striped_rounds(world, name, oracle_mod):
     got = np.concatenate([x for _, _, x in parts], axis=1)
     assert [c for c0, c1, _ in parts for c in (c0, c1)][0] == 0 and parts[-1][1] == p
     assert oracle_mod.bitwise_equal(got, ref)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_strip_kernel_never_chosen_for_halo_shards(world):
+    """the column-strip kernel stages rows 0..n-1 only, so a node shard whose rows read
+    halo rows (csr.n_in > n) must never auto-select it, even on a 64-float-multiple row stride;
+    the unsharded ring on the same stride does take it (Mixer.kernel_for, host-side only)."""
+    from niidmix.ops import Mixer
+    csr = _csr(load_golden("ring100_p257"))
+    whole = Mixer(csr=csr, device="cpu")
+    assert whole.kernel_for("fast", torch.empty(csr.n, 512)) == "strip-fast"
+    assert whole.kernel_for("exact", torch.empty(csr.n, 512)) == "strip-exact"
+    plan = ShardPlan(csr, None, world)
+    for r in range(world):
+        sh = plan.local(r)
+        assert sh.csr.n_in > sh.n_local
+        m = Mixer(csr=sh.csr, device="cpu")
+        x = torch.empty(sh.rows_in, 512)
+        for mode in ("fast", "exact"):
+            assert not m.kernel_for(mode, x).startswith("strip")
+        with pytest.raises(RuntimeError, match="strip kernel"):
+            m(x, out=torch.empty(sh.n_local, 512), kernel="strip-fast")
