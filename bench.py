@@ -13,7 +13,9 @@ already resident in HBM, ping-pong slabs.  Timed with HIP events on the stream t
 roofline: the dominant kernel's algorithmic bytes per launch (read Θ once + write Θ' once =
 2*N*P*4; gathers of neighbour rows are NOT counted) / its average launch duration (HIP events
 around every launch in the timed region), against the 8.0 TB/s HBM3E peak (MI355X_MICROARCH.md).
-Dense W (fully-connected) is priced in FLOPs (2*N^2*P) against the 157.3 TF fp32 MFMA peak.
+Dense W (fully-connected) is priced in FLOPs: kernel "dense" (bf16 splits) as 6 x 2*N^2*P bf16
+FLOPs against the ~2.5 PF bf16 MFMA peak, kernel "dense-f32" as 2*N^2*P against the 157.3 TF fp32
+MFMA peak.
 traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x2 on gfx950 + WRITE_SIZE)
 read from --traffic-json (tools/pmc_traffic.py, keyed by config.traffic_key), reported only when the
 entry was measured with the library this run loaded (config.lib_sha16), else null.
@@ -56,6 +58,9 @@ METRIC = "param-GB/s mixed (device-resident), 1000-node d-cliques, P=1M fp32"
 GRAD_METRIC = "gradient-GB/s averaged (device-resident), 1000-node d-cliques --clique-gradient, P=1M fp32"
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3
+# dense bf16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense, 16x the fp32-input MFMA rate)
+BF16_PEAK_TFLOPS = 2500.0
+B6_PRODUCTS = 6          # bf16 products per fp32 product in the split GEMM (kernel "dense")
 
 
 def parse():
@@ -69,7 +74,7 @@ def parse():
     ap.add_argument("--p", type=int, default=None, help="parameters per node (default per config)")
     ap.add_argument("--kernel", default="auto",
                     choices=["auto", "csr-exact", "csr-fast", "ell-exact", "ell-fast", "band-exact",
-                             "band-fast", "clique", "dense", "tile-exact",
+                             "band-fast", "clique", "dense", "dense-f32", "tile-exact",
                              "tile-fast", "tile-lds-exact", "tile-lds-fast"])
     ap.add_argument("--interclique", default="fully-connected",
                     choices=["fully-connected", "smallworld", "ring"],
@@ -1030,6 +1035,20 @@ def main():
                                                                             slab_layout), lib_sha)
                                 if world == 1 else (None, "multi-GPU: not profiled"))
         if kernel == "dense":
+            # the fp32 GEMM carried by bf16 splits: the matrix pipe executes B6_PRODUCTS bf16
+            # products per algorithmic fp32 one, priced against the bf16 MFMA peak; the
+            # algorithmic fp32 rate is reported beside it against the fp32 MFMA peak
+            flops = 2.0 * n_local * n_local * cols_local
+            fp32_rate = flops / (launch_ms / 1e3) / 1e12
+            achieved = B6_PRODUCTS * fp32_rate
+            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+                    "traffic": traffic,
+                    "executed": f"{B6_PRODUCTS} bf16 products per fp32 product "
+                                "(v_mfma_f32_32x32x16_bf16, three-term splits)",
+                    "fp32_equivalent_TFLOPs": round(fp32_rate, 2),
+                    "fp32_equivalent_frac_of_fp32_mfma_peak": round(fp32_rate / FP32_PEAK_TFLOPS, 4)}
+        elif kernel == "dense-f32":
             flops = 2.0 * n_local * n_local * cols_local
             achieved = flops / (launch_ms / 1e3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,

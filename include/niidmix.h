@@ -22,7 +22,10 @@
  * overlap.  Every entry point that reads one slab and writes another gets the row count and checks
  * the full extents of both (NIIDMIX_EALIAS), each slab with its own strides.
  *
- * ABI 4 (this header): niidmix_mix_band_f32 added (banded low-degree graphs, e.g. a ring in its
+ * ABI 5 (this header): niidmix_dense_split_elems / niidmix_dense_split_w /
+ * niidmix_mix_dense_bf16x6_f32 added (the dense GEMM on the bf16 matrix cores, fp32-accurate by
+ * three-term splitting); niidmix_mix_strip_f32 refuses a strip that does not fit the device's LDS.
+ * ABI 4: niidmix_mix_band_f32 added (banded low-degree graphs, e.g. a ring in its
  * cycle order), niidmix_mix_strip_f32 (column strips for few nodes), register rows in the LDS
  * tile plan.
  * ABI 3: n_rows added to niidmix_mix_tile_f32, niidmix_mix_tile_lds_f32,
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define NIIDMIX_ABI_VERSION 4
+#define NIIDMIX_ABI_VERSION 5
 
 enum niidmix_status {
     NIIDMIX_OK = 0,
@@ -325,6 +328,21 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
 int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
                           int64_t p, const float *w, const int64_t *row_ptr, const int32_t *col,
                           const float *val, void *stream);
+
+/* The same GEMM on the BF16 matrix cores with fp32 accuracy (round 5, ABI 5): each fp32 operand is
+ * split into three bf16 terms (a = a_h + a_m + a_l, residue < 2^-24 |a|) and the six partial
+ * products reaching 2^-16 |a b| are accumulated in fp32 by v_mfma_f32_32x32x16_bf16 -- on gfx950 the
+ * fp32-input MFMA runs at 1/16 of the bf16 rate, so six bf16 products cost 6/16 of one fp32 one.
+ * The error is of the order of one fp32 rounding per product (fast mode's 1e-5 condition-aware
+ * tolerance, like the fp32 kernel); non-finite outputs are recomputed from the CSR as above.
+ *   wp  the split W^T from niidmix_dense_split_w (device, 16-B aligned,
+ *       niidmix_dense_split_elems(n) uint16 elements); made once per topology.
+ * Other arguments as niidmix_mix_dense_f32. */
+int64_t niidmix_dense_split_elems(int64_t n);
+int niidmix_dense_split_w(const float *w, int64_t n, uint16_t *wp, void *stream);
+int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
+                                 int64_t p, const uint16_t *wp, const int64_t *row_ptr,
+                                 const int32_t *col, const float *val, void *stream);
 
 /* Column mean over rows (the uniform global average of setup.model.average(models) with
  * weights=None, model/__init__.py:17-18, used by d_sgd.init :137-141 and the logger :112,260),

@@ -1265,6 +1265,197 @@ __global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict_
 }
 
 // ----------------------------------------------------------------------------------------------
+// Dense Y = W^T X on the BF16 matrix cores, fp32-accurate by three-term splitting (round 5).
+// On gfx950 the fp32-input MFMA issues at 1/16 of the bf16 rate (64 vs 1024 FLOP/clk/SIMD,
+// MI355X_MICROARCH.md § Matrix cores), so an fp32 product a*b is carried by bf16 splits
+// a = a_h + a_m + a_l (a_h = RNE bf16 of a, a_m of a - a_h, a_l of a - a_h - a_m; the residue is below
+// 2^-24 |a|) and the six partial products that reach 2^-16 |a b| are summed in fp32 by the MFMA:
+//     a_h b_h + a_h b_m + a_m b_h + a_h b_l + a_l b_h + a_m b_m.
+// The dropped terms (a_m b_l, a_l b_m, a_l b_l) and the residues stay below ~2^-23 |a b| -- the order
+// of one fp32 rounding -- so the result keeps fast mode's 1e-5 condition-aware tolerance with an
+// fp32 GEMM's margin, at 16/6 = 2.7x the fp32 MFMA's rate.  Non-finite inputs make the splits NaN
+// (inf - inf) and the output non-finite, which the guard recomputes from the CSR (as k_mix_dense).
+//   W^T is split ONCE per topology (k_dense_split_w): wp[3][mpad][kpad] bf16, row i = output node,
+//   k contiguous, zero-padded (mpad = n rounded up to 128, kpad to 16).
+//   X is split as it is staged: LDS [plane][column][16 k] bf16, so a B operand's run of 8 k is one
+//   ds_read_b128; W tiles land in LDS [plane][row][16 k] the same way.
+// Block tile 128 rows x 256 columns, 8 waves (2 x 4), each 64 x 64 = 2 x 2 accumulators of
+// v_mfma_f32_32x32x16_bf16; K-step 16, LDS double-buffered (72 KB dynamic), the next K-step's W
+// pieces and X values fetched into registers during the MFMAs, one barrier per K-step.  Operand
+// maps (32x32x16 bf16): lane l holds A[l&31][8(l>>5) + 0..7] and B[8(l>>5) + 0..7][l&31]; C as
+// k_mix_dense.  The two 16-B halves of every 32-B LDS row swap places on alternate groups of 8
+// rows (half ^ (row >> 3 & 1)): the ds_read_b128 of 16 consecutive rows hit 16 distinct bank quads.
+constexpr int kB6M = 128, kB6N = 256, kB6K = 16;
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+// two floats -> their three bf16 split planes, each as a packed pair (first value in the low half)
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
+    const bf16x2v hv = {(__bf16)a, (__bf16)b};
+    const uint32_t hb = __builtin_bit_cast(uint32_t, hv);
+    const float ra = a - __builtin_bit_cast(float, hb << 16);
+    const float rb = b - __builtin_bit_cast(float, hb & 0xffff0000u);
+    const bf16x2v mv = {(__bf16)ra, (__bf16)rb};
+    const uint32_t mb = __builtin_bit_cast(uint32_t, mv);
+    const float sa = ra - __builtin_bit_cast(float, mb << 16);
+    const float sb = rb - __builtin_bit_cast(float, mb & 0xffff0000u);
+    const bf16x2v lv = {(__bf16)sa, (__bf16)sb};
+    h = hb;
+    m = mb;
+    l = __builtin_bit_cast(uint32_t, lv);
+}
+
+// wp[p][i][k] = plane p of W[k][i] = w[k * n + i]; zero outside [n, n)
+__global__ __launch_bounds__(256) void k_dense_split_w(const float *__restrict__ w, int64_t n,
+                                                       int64_t mpad, int64_t kpad,
+                                                       uint32_t *__restrict__ wp) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // k pair index
+    const int64_t half = kpad / 2;
+    if (q >= mpad * half) return;
+    const int64_t i = q / half, k = 2 * (q - i * half);
+    const float a = (i < n && k < n) ? w[k * n + i] : 0.f;
+    const float b = (i < n && k + 1 < n) ? w[(k + 1) * n + i] : 0.f;
+    uint32_t h, m, l;
+    split3_pair(a, b, h, m, l);
+    const int64_t plane = mpad * half;                  // uint32 words per plane
+    wp[q] = h;
+    wp[plane + q] = m;
+    wp[2 * plane + q] = l;
+}
+
+__global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
+    int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
+    int64_t n_items, const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
+    const float *__restrict__ csr_val) {
+    extern __shared__ uint4 lds_b6[];
+    // As[buf][plane][row][half] then Bs[buf][plane][col][half], 16 B each
+    auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
+        return lds_b6[((b * 3 + pl) * kB6M + row) * 2 + hf];
+    };
+    auto B_at = [&](int b, int pl, int col, int hf) -> uint4 & {
+        return lds_b6[2 * 3 * kB6M * 2 + ((b * 3 + pl) * kB6N + col) * 2 + hf];
+    };
+    const int tid = threadIdx.x;
+    const int wave = wave_id();
+    const int lane = tid & 63;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int bj = tid & (kB6N - 1), bh = tid >> 8;        // X loader: column, k half
+    const int hl = lane >> 5;
+    const int64_t S = kpad / kB6K;
+    const int64_t plane_el = mpad * kpad;                  // bf16 elements per W plane
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t jt = (local / n_it) * 8 + xcd;
+        const int64_t it = local % n_it;
+        const int64_t i0 = it * kB6M, j0 = jt * kB6N;
+        if (j0 >= p) continue;                             // block-uniform
+        floatx16 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        uint4 ra[2];
+        float rb[8];
+        const int64_t jx = j0 + bj;
+        const bool jin = jx < p;
+        auto fetch = [&](int64_t s) {
+            const int64_t k0 = s * kB6K;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = tid + 512 * u;               // 768 pieces: 3 planes x 128 rows x 2
+                if (q < 3 * kB6M * 2) {
+                    const int pl = q >> 8, row = (q >> 1) & (kB6M - 1), hf = q & 1;
+                    ra[u] = *reinterpret_cast<const uint4 *>(
+                        wp + pl * plane_el + (i0 + row) * kpad + k0 + 8 * hf);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t k = k0 + 8 * bh + u;
+                rb[u] = (k < n && jin) ? x[k * ld_x + jx] : 0.f;
+            }
+        };
+        auto stash = [&](int b) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = tid + 512 * u;
+                if (q < 3 * kB6M * 2) {
+                    const int pl = q >> 8, row = (q >> 1) & (kB6M - 1), hf = q & 1;
+                    A_at(b, pl, row, hf ^ ((row >> 3) & 1)) = ra[u];
+                }
+            }
+            uint32_t h[4], m[4], l[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) split3_pair(rb[2 * u], rb[2 * u + 1], h[u], m[u], l[u]);
+            const int sh = bh ^ ((bj >> 3) & 1);
+            B_at(b, 0, bj, sh) = make_uint4(h[0], h[1], h[2], h[3]);
+            B_at(b, 1, bj, sh) = make_uint4(m[0], m[1], m[2], m[3]);
+            B_at(b, 2, bj, sh) = make_uint4(l[0], l[1], l[2], l[3]);
+        };
+        fetch(0);
+        stash(0);
+        __syncthreads();
+        for (int64_t s = 0; s < S; ++s) {
+            const int b = (int)(s & 1);
+            if (s + 1 < S) fetch(s + 1);                   // in flight during the MFMAs below
+            bf16x8v af[2][3], bf[2][3];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int row = wm * 64 + a * 32 + (lane & 31);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    af[a][pl] = __builtin_bit_cast(bf16x8v, A_at(b, pl, row, hl ^ ((row >> 3) & 1)));
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int col = wn * 64 + c * 32 + (lane & 31);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    bf[c][pl] = __builtin_bit_cast(bf16x8v, B_at(b, pl, col, hl ^ ((col >> 3) & 1)));
+            }
+            // the six split products, smallest first, each over the 2 x 2 accumulators
+            constexpr int PA[6] = {1, 2, 0, 1, 0, 0}, PB[6] = {1, 0, 2, 0, 1, 0};
+#pragma unroll
+            for (int e = 0; e < 6; ++e)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][PA[e]], bf[c][PB[e]],
+                                                                            acc[a][c], 0, 0, 0);
+            if (s + 1 < S) stash(b ^ 1);
+            __syncthreads();
+        }
+        uint64_t bad = 0;                                  // this lane's non-finite outputs
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
+                    if (i < n && j < p) {
+                        if (__builtin_isfinite(acc[a][c][r])) __builtin_nontemporal_store(acc[a][c][r], y + i * ld_y + j);
+                        else bad |= 1ull << (a * 32 + c * 16 + r);
+                    }
+                }
+        while (bad) {                                      // non-finite guard (csr_refix1)
+            const int q = __builtin_ctzll(bad);
+            bad &= bad - 1;
+            const int a = q >> 5, c = (q >> 4) & 1, r = q & 15;
+            const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
+            __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // Clique-factored mixing for BIG cliques (> 256 members, e.g. a fully-connected topology with MH
 // weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), WAVES waves, lane =
 // one column.  Pass 1 streams the members (wave w: a contiguous 1/WAVES of them) into per-group
@@ -3915,6 +4106,51 @@ int niidmix_mix_dense_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, 
     else     { if (avec) NIIDMIX_DENSE(false, true); else NIIDMIX_DENSE(false, false); }
 #undef NIIDMIX_DENSE
     return check_launch("k_mix_dense");
+}
+
+int64_t niidmix_dense_split_elems(int64_t n) {
+    if (n <= 0) return 0;
+    const int64_t mpad = (n + kB6M - 1) / kB6M * kB6M, kpad = (n + kB6K - 1) / kB6K * kB6K;
+    return 3 * mpad * kpad;
+}
+
+int niidmix_dense_split_w(const float *w, int64_t n, uint16_t *wp, void *stream) {
+    if (n < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n == 0) return NIIDMIX_OK;
+    if (!w || !wp) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (reinterpret_cast<uintptr_t>(wp) & 15) return set_error(NIIDMIX_EUNSUPPORTED, "wp not 16-B aligned");
+    const int64_t mpad = (n + kB6M - 1) / kB6M * kB6M, kpad = (n + kB6K - 1) / kB6K * kB6K;
+    if (overlaps(w, n * n, reinterpret_cast<const float *>(wp), 3 * mpad * kpad / 2))
+        return set_error(NIIDMIX_EALIAS, "w and wp overlap");
+    const int64_t pairs = mpad * kpad / 2;
+    hipLaunchKernelGGL(k_dense_split_w, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), w, n, mpad, kpad,
+                       reinterpret_cast<uint32_t *>(wp));
+    return check_launch("k_dense_split_w");
+}
+
+int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t n,
+                                 int64_t p, const uint16_t *wp, const int64_t *row_ptr,
+                                 const int32_t *col, const float *val, void *stream) {
+    if (n < 0 || p < 0) return set_error(NIIDMIX_EINVAL, "negative size");
+    if (n == 0 || p == 0) return NIIDMIX_OK;
+    if (!x || !y || !wp || !row_ptr || !col || !val) return set_error(NIIDMIX_EINVAL, "null pointer");
+    if (ld_x < p || ld_y < p) return set_error(NIIDMIX_EINVAL, "leading dimension < p");
+    if (reinterpret_cast<uintptr_t>(wp) & 15) return set_error(NIIDMIX_EUNSUPPORTED, "wp not 16-B aligned");
+    if (overlaps(x, (n - 1) * ld_x + p, y, (n - 1) * ld_y + p))
+        return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t mpad = (n + kB6M - 1) / kB6M * kB6M, kpad = (n + kB6K - 1) / kB6K * kB6K;
+    const int64_t n_it = mpad / kB6M;
+    const int64_t n_jt = (p + kB6N - 1) / kB6N;
+    const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
+    const size_t lds = (size_t)2 * 3 * (kB6M + kB6N) * 2 * sizeof(uint4);    // 72 KB
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return set_error(NIIDMIX_EHIP, "k_mix_dense_b6: %zu B of LDS refused", lds);
+    hipLaunchKernelGGL(k_mix_dense_b6, dim3((unsigned)grid_for(n_items)), dim3(512), lds, s, x, ld_x,
+                       y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val);
+    return check_launch("k_mix_dense_b6");
 }
 
 int niidmix_mean_rows_f32(const float *x, int64_t ld_x, int64_t n, int64_t p, float *mean,

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NIIDMIX_LIB") or os.path.join(_HERE, "libniidmix.so")
 
 OK, EINVAL, EALIAS, EHIP, EUNSUPPORTED = 0, 1, 2, 3, 4
 MODE_EXACT, MODE_FAST = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _i64, _i32, _vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
 
@@ -76,6 +76,10 @@ SIGNATURES = {
                                                 ctypes.POINTER(TileLdsPlanC), ctypes.c_int, _vp]),
     "niidmix_mix_dense_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
                                              _vp, _vp]),
+    "niidmix_dense_split_elems": (_i64, [_i64]),
+    "niidmix_dense_split_w": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
+    "niidmix_mix_dense_bf16x6_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
+                                                    _vp, _vp]),
     "niidmix_mean_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_int, _vp]),
     "niidmix_grad_segment_mean_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp,
                                                      _vp, _vp]),

@@ -14,6 +14,7 @@ Ops (registered in the `niidmix` namespace, usable as torch.ops.niidmix.*):
   mix_tile_lds(x, <tile lds plan tensors>, out, rt, max_src, max_tiles, mode)
                                                     k_mix_tile_lds (exact default, LDS-staged)
   mix_dense(x, w, row_ptr, col, val, out)           k_mix_dense  (fp32 MFMA; CSR = non-finite guard)
+  mix_dense_b6(x, wp, row_ptr, col, val, out)       k_mix_dense_b6 (bf16 MFMA, fp32-accurate splits)
   mean_rows(x, mean, dist2, mode)                   k_mean_cols + k_row_dist2
   grad_segment_mean(g, seg_ptr, seg_row, out)       k_grad_segment_mean (clique gradient mean)
   sgd_step_rows(p, g, rows, neg_lr)                 k_sgd_step_rows (the optimizer step, fused round)
@@ -424,6 +425,39 @@ def mix_dense(x: torch.Tensor, w: torch.Tensor, row_ptr: torch.Tensor, col: torc
     _lib.check(rc, "niidmix::mix_dense")
 
 
+def dense_split_w(w: torch.Tensor) -> torch.Tensor:
+    """W^T split into three bf16 planes for mix_dense_b6 (niidmix_dense_split_w): uint16 storage of
+    niidmix_dense_split_elems(n) elements on w's device, made once per topology."""
+    _req(w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.shape[0] == w.shape[1]
+         and w.is_contiguous(), "w: expected contiguous fp32 [N, N] on a HIP device")
+    n = w.shape[0]
+    wp = torch.empty(int(_lib.lib.niidmix_dense_split_elems(n)), dtype=torch.int16, device=w.device)
+    rc = _lib.lib.niidmix_dense_split_w(w.data_ptr(), n, wp.data_ptr(), _stream(w))
+    _lib.check(rc, "niidmix::dense_split_w")
+    return wp
+
+
+@torch.library.custom_op("niidmix::mix_dense_b6", mutates_args=("out",))
+def mix_dense_b6(x: torch.Tensor, wp: torch.Tensor, row_ptr: torch.Tensor, col: torch.Tensor,
+                 val: torch.Tensor, out: torch.Tensor) -> None:
+    """Y = W^T X on the bf16 matrix cores with fp32 accuracy (three-term splits, six products;
+    include/niidmix.h niidmix_mix_dense_bf16x6_f32); wp from dense_split_w."""
+    _slab("x", x)
+    n = x.shape[0]
+    _slab("out", out, rows=n, cols=x.shape[1])
+    _req(wp.device == x.device and wp.dtype == torch.int16 and wp.is_contiguous() and
+         wp.numel() == int(_lib.lib.niidmix_dense_split_elems(n)),
+         "wp: expected the dense_split_w planes of an [N, N] W")
+    _vec("row_ptr", row_ptr, torch.int64, x.device, n + 1)
+    _vec("col", col, torch.int32, x.device)
+    _vec("val", val, torch.float32, x.device, col.numel())
+    _no_overlap(x, out)
+    rc = _lib.lib.niidmix_mix_dense_bf16x6_f32(x.data_ptr(), _ld(x), out.data_ptr(), _ld(out), n,
+                                               x.shape[1], wp.data_ptr(), row_ptr.data_ptr(),
+                                               col.data_ptr(), val.data_ptr(), _stream(x))
+    _lib.check(rc, "niidmix::mix_dense_b6")
+
+
 @torch.library.custom_op("niidmix::mean_rows", mutates_args=("mean", "dist2"))
 def mean_rows(x: torch.Tensor, mean: torch.Tensor, dist2: torch.Tensor, mode: int) -> None:
     _slab("x", x)
@@ -517,7 +551,7 @@ _LAZY = {
     "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
     "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
     "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds", "l_rem_rows": "tlds",
-    "w_dense": "dense",
+    "w_dense": "dense", "w_split": "dense",
     "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell", "band": "ell",
 }
 
@@ -744,6 +778,8 @@ class Mixer:
 
     def _build_dense(self):
         self.w_dense = torch.from_numpy(self.csr.dense()).to(self.device)
+        # W^T split into bf16 planes once per topology (the bf16x6 GEMM, kernel "dense")
+        self.w_split = dense_split_w(self.w_dense) if self.w_dense.is_cuda else None
 
     def device_layout(self):
         """(perm, block_cols): the device-resident layout the factored kernels stream best, measured
@@ -907,6 +943,9 @@ class Mixer:
             mix_clique(x, *self._clique_args(), out, self.plan.max_clique,
                        self.plan.max_clique_res)
         elif k == "dense":
+            # bf16 matrix cores, fp32-accurate by three-term splits: 2.7x the fp32 MFMA's rate
+            mix_dense_b6(x, self.w_split, self.row_ptr, self.col, self.val, out)
+        elif k == "dense-f32":
             mix_dense(x, self.w_dense, self.row_ptr, self.col, self.val, out)
         else:
             raise ValueError(f"unknown kernel {k!r}")

@@ -9,7 +9,7 @@ from conftest import REPO
 
 def _declared_symbols():
     text = open(os.path.join(REPO, "include", "niidmix.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void \*|void)\s*(niidmix_\w+)\s*\(",
+    return sorted(set(re.findall(r"^\s*(?:int64_t|int|const char \*|void \*|void)\s*(niidmix_\w+)\s*\(",
                                  text, re.M)))
 
 
@@ -73,6 +73,17 @@ def test_argument_errors_without_gpu():
     assert rc == _lib.EALIAS         # x starts inside y
     rc = L.niidmix_mix_dense_f32(16, 4, 1024, 4, 4, 4, 8, None, 8, 8, None)
     assert rc == _lib.EINVAL         # dense: the CSR (non-finite guard) is required
+    # ABI 5: the bf16x6 dense GEMM and its W split
+    assert L.niidmix_dense_split_elems(1000) == 3 * 1024 * 1008
+    assert L.niidmix_dense_split_elems(0) == 0
+    rc = L.niidmix_mix_dense_bf16x6_f32(16, 4, 1024, 4, 4, 4, 16, None, 8, 8, None)
+    assert rc == _lib.EINVAL         # the CSR (non-finite guard) is required
+    rc = L.niidmix_mix_dense_bf16x6_f32(16, 4, 1024, 4, 4, 4, 8, 8, 8, 8, None)
+    assert rc == _lib.EUNSUPPORTED   # split W must be 16-B aligned
+    rc = L.niidmix_mix_dense_bf16x6_f32(base, 8, base + 4 * 20, 8, 4, 8, 1 << 24, 8, 8, 8, None)
+    assert rc == _lib.EALIAS
+    rc = L.niidmix_dense_split_w(4096, 4, 4096 + 16, None)
+    assert rc == _lib.EALIAS         # w and its split overlap
     tp = _lib.TilePlanC(1, 12, 0, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 1, 4, ctypes.byref(tp), 0, None)
     assert rc == _lib.EUNSUPPORTED   # tile height 12

@@ -41,7 +41,8 @@ def test_exact_kernel_bitwise_vs_golden(name, kernel, gpu, oracle_mod):
 
 
 @pytest.mark.parametrize("name", golden_cases())
-@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "tile-fast", "ell-fast"])
+@pytest.mark.parametrize("kernel", ["csr-fast", "clique", "dense", "dense-f32", "tile-fast",
+                                    "ell-fast"])
 def test_fast_kernels_tolerance_vs_golden(name, kernel, gpu, oracle_mod):
     """Every fast kernel on every golden case, non-finite fixtures included: NaN where the
     reference has NaN, the same inf where it has inf (the factored and GEMM kernels recompute
@@ -430,7 +431,7 @@ def test_mean_rows_and_distance(gpu, oracle_mod):
     assert oracle_mod.bitwise_equal(mean[:4096].cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("kernel", ["dense", "clique"])
+@pytest.mark.parametrize("kernel", ["dense", "dense-f32", "clique"])
 def test_fc1000_dense_and_factored(kernel, gpu, oracle_mod):
     """configs[3] shape (fully-connected N=1000, MH weights) at reduced P: the MFMA GEMM and the
     big-clique factored kernel (two-pass) both within the tolerance of the oracle."""
@@ -466,7 +467,7 @@ def test_dense_kstep_variants_agree(gpu, oracle_mod, monkeypatch):
     for bk, occ in (("16", "3"), ("32", "0"), ("8", "3"), ("8", "4"), ("16", "4")):
         monkeypatch.setenv("NIIDMIX_DENSE_BK", bk)
         monkeypatch.setenv("NIIDMIX_DENSE_OCC", occ)
-        outs[(bk, occ)] = m(x, kernel="dense").cpu().numpy()
+        outs[(bk, occ)] = m(x, kernel="dense-f32").cpu().numpy()
     base = outs[("16", "3")]
     for k, y in outs.items():
         assert oracle_mod.bitwise_equal(y, base), k
@@ -730,3 +731,37 @@ def test_tile_lds_register_rows_vs_golden(name, mode, regs, gpu, oracle_mod, mon
         bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
         ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
         assert ok, (name, worst)
+
+
+@pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (130, 257), (257, 1030), (17, 5)])
+def test_dense_b6_split_gemm(n, p, gpu, oracle_mod):
+    """The bf16x6 dense GEMM (kernel "dense": three-term bf16 splits, six products on
+    v_mfma_f32_32x32x16_bf16) on a dense column-stochastic W with no structure, ragged M, K and P
+    (partial 128-row and 256-column tiles, K not a multiple of 16, odd P): within the 1e-5
+    condition-aware tolerance of the oracle, and no worse than 4x the fp32 MFMA kernel's worst
+    relative error on the same inputs (the split keeps fp32-level accuracy)."""
+    ops = _ops()
+    rng = np.random.default_rng(n + p)
+    w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)
+    w /= w.sum(0, keepdims=True)
+    csr = ops.csr_from_numpy(*_dense_csr(w))
+    m = ops.Mixer(csr=csr, device=gpu)
+    x = torch.from_numpy(rng.standard_normal((n, p)).astype(np.float32) * 3).to(gpu)
+    xn = x.cpu().numpy()
+    ref = oracle_mod.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
+    bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
+    worst = {}
+    for k in ("dense", "dense-f32"):
+        y = m(x, kernel=k).cpu().numpy()
+        ok, worst[k] = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+        assert ok, (k, worst[k])
+    assert worst["dense"] <= 4 * max(worst["dense-f32"], 1e-7), worst
+
+
+def _dense_csr(w):
+    """CSR of W^T rows (self first) of a dense [N, N] W (every entry an edge)."""
+    n = w.shape[0]
+    row_ptr = np.arange(n + 1, dtype=np.int64) * n
+    col = np.concatenate([[i] + [j for j in range(n) if j != i] for i in range(n)]).astype(np.int32)
+    val = w[col, np.repeat(np.arange(n), n)].astype(np.float32)
+    return row_ptr, col, val
