@@ -37,6 +37,7 @@
 
 #include <mutex>
 #include <unordered_map>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/niidmix.h"
@@ -1286,6 +1287,8 @@ __global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict_
 // k_mix_dense.  The two 16-B halves of every 32-B LDS row swap places on alternate groups of 8
 // rows (half ^ (row >> 3 & 1)): the ds_read_b128 of 16 consecutive rows hit 16 distinct bank quads.
 constexpr int kB6M = 128, kB6N = 256, kB6K = 16;
+// the six split products (plane of A, plane of B), smallest first: mm, lh, hl, mh, hm, hh
+__device__ constexpr int kB6PA[6] = {1, 2, 0, 1, 0, 0}, kB6PB[6] = {1, 0, 2, 0, 1, 0};
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
@@ -1341,6 +1344,12 @@ __global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
     const int lane = tid & 63;
     const int wm = wave >> 2, wn = wave & 3;
     const int bj = tid & (kB6N - 1), bh = tid >> 8;        // X loader: column, k half
+    // W loader: pieces q0 = tid and q1 = tid + 512 of 768 (3 planes x 128 rows x 2 halves); the
+    // threads past 768 load piece q1 - 256 again and do not store it
+    const int q0pl = tid >> 8, q0row = (tid >> 1) & (kB6M - 1), q0hf = tid & 1;
+    const bool q1ok = tid + 512 < 3 * kB6M * 2;
+    const int q1 = q1ok ? tid + 512 : tid + 256;
+    const int q1pl = q1 >> 8, q1row = (q1 >> 1) & (kB6M - 1), q1hf = q1 & 1;
     const int hl = lane >> 5;
     const int64_t S = kpad / kB6K;
     const int64_t plane_el = mpad * kpad;                  // bf16 elements per W plane
@@ -1358,78 +1367,91 @@ __global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
             for (int b = 0; b < 2; ++b)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-        uint4 ra[2];
-        float rb[8];
+        // Two register sets of prefetched operands (K-steps s + 1 and s + 2): the loads of a K-step
+        // are issued two steps before it is computed and split one step before, interleaved with
+        // the MFMAs of the step in between.  Every load is unconditional (clamped addresses; the X
+        // values past n or p are zeroed by a bit mask after the load, never by a branch): the
+        // number of loads in flight is the same on every path, so each split waits only for its
+        // own loads.  Written as macros over named registers (no arrays behind a lambda's
+        // reference capture, which hipcc put in scratch memory).
         const int64_t jx = j0 + bj;
         const bool jin = jx < p;
-        auto fetch = [&](int64_t s) {
-            const int64_t k0 = s * kB6K;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int q = tid + 512 * u;               // 768 pieces: 3 planes x 128 rows x 2
-                if (q < 3 * kB6M * 2) {
-                    const int pl = q >> 8, row = (q >> 1) & (kB6M - 1), hf = q & 1;
-                    ra[u] = *reinterpret_cast<const uint4 *>(
-                        wp + pl * plane_el + (i0 + row) * kpad + k0 + 8 * hf);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t k = k0 + 8 * bh + u;
-                rb[u] = (k < n && jin) ? x[k * ld_x + jx] : 0.f;
-            }
-        };
-        auto stash = [&](int b) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int q = tid + 512 * u;
-                if (q < 3 * kB6M * 2) {
-                    const int pl = q >> 8, row = (q >> 1) & (kB6M - 1), hf = q & 1;
-                    A_at(b, pl, row, hf ^ ((row >> 3) & 1)) = ra[u];
-                }
-            }
-            uint32_t h[4], m[4], l[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) split3_pair(rb[2 * u], rb[2 * u + 1], h[u], m[u], l[u]);
-            const int sh = bh ^ ((bj >> 3) & 1);
-            B_at(b, 0, bj, sh) = make_uint4(h[0], h[1], h[2], h[3]);
-            B_at(b, 1, bj, sh) = make_uint4(m[0], m[1], m[2], m[3]);
-            B_at(b, 2, bj, sh) = make_uint4(l[0], l[1], l[2], l[3]);
-        };
-        fetch(0);
-        stash(0);
+        const int64_t jc = jin ? jx : p - 1;
+        const float *xcol = x + jc;
+        const uint16_t *wpa = wp + (int64_t)q0pl * plane_el + (i0 + q0row) * kpad + 8 * q0hf;
+        const uint16_t *wpb = wp + (int64_t)q1pl * plane_el + (i0 + q1row) * kpad + 8 * q1hf;
+        uint4 wa0, wb0, wa1, wb1;
+        float xv0[8], xv1[8];
+        // the X rows a wave loads (k0 + 8 bh + u) are wave-uniform: scalar row addresses, one
+        // 32-bit lane offset (the column)
+        const int bhu = __builtin_amdgcn_readfirstlane(bh);
+        const uint32_t xoff = (uint32_t)jc * 4u;
+#define B6_FETCH(SET, S_)                                                                          \
+        do {                                                                                       \
+            const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
+            wa##SET = *reinterpret_cast<const uint4 *>(wpa + k0_);                                \
+            wb##SET = *reinterpret_cast<const uint4 *>(wpb + k0_);                                \
+            _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                        \
+                const int64_t k_ = k0_ + 8 * bhu + u;                                              \
+                const char *row_ = reinterpret_cast<const char *>(x + (k_ < n ? k_ : n - 1) * ld_x); \
+                xv##SET[u] = *reinterpret_cast<const float *>(row_ + xoff);                       \
+            }                                                                                      \
+        } while (0)
+        // the split zeroes X past n rows or p columns (clamped loads above) by a bit mask, here,
+        // where the values are used -- not right behind the loads, which would wait for them
+#define B6_STASH(SET, BUF, S_)                                                                     \
+        do {                                                                                       \
+            A_at(BUF, q0pl, q0row, q0hf ^ ((q0row >> 3) & 1)) = wa##SET;                           \
+            if (q1ok) A_at(BUF, q1pl, q1row, q1hf ^ ((q1row >> 3) & 1)) = wb##SET;                 \
+            float xm_[8];                                                                          \
+            _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                        \
+                const int64_t k_ = (S_) * kB6K + 8 * bhu + u;                                      \
+                const uint32_t m_ = (k_ < n && jin) ? 0xffffffffu : 0u;                             \
+                xm_[u] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, xv##SET[u]) & m_); \
+            }                                                                                      \
+            uint32_t h_[4], m_[4], l_[4];                                                          \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u)                                          \
+                split3_pair(xm_[2 * u], xm_[2 * u + 1], h_[u], m_[u], l_[u]);                      \
+            const int sh_ = bh ^ ((bj >> 3) & 1);                                                  \
+            B_at(BUF, 0, bj, sh_) = make_uint4(h_[0], h_[1], h_[2], h_[3]);                        \
+            B_at(BUF, 1, bj, sh_) = make_uint4(m_[0], m_[1], m_[2], m_[3]);                        \
+            B_at(BUF, 2, bj, sh_) = make_uint4(l_[0], l_[1], l_[2], l_[3]);                        \
+        } while (0)
+        // K-step s on LDS buffer B = s & 1: issue the loads of s + 2 (register set B), read the
+        // operands, run the MFMAs, split s + 1 (set B ^ 1) into buffer B ^ 1, barrier
+#define B6_STEP(B, NB, S_)                                                                         \
+        do {                                                                                       \
+            B6_FETCH(B, (S_) + 2);                                                                 \
+            bf16x8v af_[2][3], bf_[2][3];                                                          \
+            _Pragma("unroll") for (int a = 0; a < 2; ++a) {                                        \
+                const int row_ = wm * 64 + a * 32 + (lane & 31);                                   \
+                _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                   \
+                    af_[a][pl] = __builtin_bit_cast(bf16x8v, A_at(B, pl, row_, hl ^ ((row_ >> 3) & 1))); \
+            }                                                                                      \
+            _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                        \
+                const int col_ = wn * 64 + c * 32 + (lane & 31);                                   \
+                _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                   \
+                    bf_[c][pl] = __builtin_bit_cast(bf16x8v, B_at(B, pl, col_, hl ^ ((col_ >> 3) & 1))); \
+            }                                                                                      \
+            _Pragma("unroll") for (int e = 0; e < 6; ++e)                                          \
+                _Pragma("unroll") for (int a = 0; a < 2; ++a)                                      \
+                    _Pragma("unroll") for (int c = 0; c < 2; ++c)                                  \
+                        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
+                            af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
+            if ((S_) + 1 < S) B6_STASH(NB, NB, (S_) + 1);                                          \
+            __syncthreads();                                                                       \
+        } while (0)
+        B6_FETCH(0, 0);
+        B6_STASH(0, 0, 0);
+        B6_FETCH(1, 1);
         __syncthreads();
-        for (int64_t s = 0; s < S; ++s) {
-            const int b = (int)(s & 1);
-            if (s + 1 < S) fetch(s + 1);                   // in flight during the MFMAs below
-            bf16x8v af[2][3], bf[2][3];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const int row = wm * 64 + a * 32 + (lane & 31);
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-                    af[a][pl] = __builtin_bit_cast(bf16x8v, A_at(b, pl, row, hl ^ ((row >> 3) & 1)));
-            }
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int col = wn * 64 + c * 32 + (lane & 31);
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-                    bf[c][pl] = __builtin_bit_cast(bf16x8v, B_at(b, pl, col, hl ^ ((col >> 3) & 1)));
-            }
-            // the six split products, smallest first, each over the 2 x 2 accumulators
-            constexpr int PA[6] = {1, 2, 0, 1, 0, 0}, PB[6] = {1, 0, 2, 0, 1, 0};
-#pragma unroll
-            for (int e = 0; e < 6; ++e)
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][PA[e]], bf[c][PB[e]],
-                                                                            acc[a][c], 0, 0, 0);
-            if (s + 1 < S) stash(b ^ 1);
-            __syncthreads();
+        for (int64_t s = 0; s < S; s += 2) {
+            B6_STEP(0, 1, s);
+            if (s + 1 < S) B6_STEP(1, 0, s + 1);
         }
+#undef B6_STEP
+#undef B6_STASH
+#undef B6_FETCH
         uint64_t bad = 0;                                  // this lane's non-finite outputs
 #pragma unroll
         for (int a = 0; a < 2; ++a)
