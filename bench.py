@@ -421,11 +421,60 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             out["host_blocked_ms"] = round(st["blocked"] / rounds * 1e3, 2)
             out["host_wait_ms"] = round(st["wait"] / rounds * 1e3, 2)
         res[v] = out
+    res["logger"] = e2e_logger_costs([nd["model"] for nd in sts["row_streamed"]["nodes"]])
     d_sgd._engines.clear()
     d_sgd._fused_engines.clear()
     del sts
     torch.cuda.empty_cache()
     return res
+
+
+def e2e_logger_costs(models, reps=3, cpu_sample=50):
+    """What run.py's logging costs after a round at this size, with the hooks
+    niidmix.d_sgd.init installs (niidmix.logger): the consensus-distance statistics and the global
+    model (setup.model.average over every node) read from the resident output slab; the consensus
+    statistics again from the pinned host slab (one H2D, the path before the first round or after a
+    guarded write); and the reference's CPU arithmetic (logger.py:257-284: fp32 centre, one
+    model_distance per model) timed on the first `cpu_sample` models and scaled to all of them."""
+    from niidmix import guard
+    from niidmix import logger as nl
+    hit = guard.resident_rows(models)
+    if hit is None or not hit[0].fresh:
+        return {"error": "no fresh resident slab after the rounds"}
+    rr = hit[0]
+
+    def med(fn):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return round(float(np.median(ts)) * 1e3, 2)
+    out = {"consensus_resident_ms": med(lambda: nl.consensus_statistics(models)),
+           "consensus_source": nl.last_source["consensus"],
+           "global_average_resident_ms": med(lambda: nl.average(models)),
+           "average_source": nl.last_source["average"]}
+    rr.fresh = False
+    try:
+        out["consensus_host_slab_ms"] = med(lambda: nl.consensus_statistics(models))
+        out["host_slab_source"] = nl.last_source["consensus"]
+    finally:
+        rr.fresh = True
+    sample = models[:cpu_sample]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        flat = [torch.cat([q.detach().reshape(-1) for q in m.parameters()]) for m in sample]
+        w = float(1. / len(models))
+        center = flat[0] * 0
+        for f in flat:
+            center = center + w * f
+        _ = [float(torch.sum((center - f) ** 2)) for f in flat]
+    out["consensus_cpu_reference_ms_scaled"] = round((time.perf_counter() - t0) * 1e3 *
+                                                     len(models) / len(sample), 1)
+    out["cpu_sample_models"] = len(sample)
+    return out
 
 
 def traffic_key(args, kernel, p, slab_layout):
