@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict_
 // maps (32x32x16 bf16): lane l holds A[l&31][8(l>>5) + 0..7] and B[8(l>>5) + 0..7][l&31]; C as
 // k_mix_dense.  The two 16-B halves of every 32-B LDS row swap places on alternate groups of 8
 // rows (half ^ (row >> 3 & 1)): the ds_read_b128 of 16 consecutive rows hit 16 distinct bank quads.
-constexpr int kB6M = 128, kB6N = 256, kB6K = 16;
+constexpr int kB6M = 128, kB6K = 16;
 // the six split products (plane of A, plane of B), smallest first: mm, lh, hl, mh, hm, hh
 __device__ constexpr int kB6PA[6] = {1, 2, 0, 1, 0, 0}, kB6PB[6] = {1, 0, 2, 0, 1, 0};
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -1326,30 +1326,45 @@ __global__ __launch_bounds__(256) void k_dense_split_w(const float *__restrict__
     wp[2 * plane + q] = l;
 }
 
-__global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
+// WN = waves along N: 4 -> 8-wave blocks of 128 x 256 (one block per CU: 176 VGPRs, 2 waves per
+// SIMD, one barrier phase per CU), 2 -> 4-wave blocks of 128 x 128 (two blocks per CU, each with
+// its own barrier phase, so one block's split and barrier overlap the other's MFMAs; W is re-read
+// per 128 columns instead of 256)
+template <int WN, int SCHED>
+__global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
     int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
     int64_t n_items, const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
     const float *__restrict__ csr_val) {
+    constexpr int NT = 128 * WN;                           // threads
+    constexpr int BN = 64 * WN;                            // columns per block tile
+    constexpr int NPIECE = 3 * kB6M * 2;                   // 16-B W pieces per K-step (768)
     extern __shared__ uint4 lds_b6[];
     // As[buf][plane][row][half] then Bs[buf][plane][col][half], 16 B each
     auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
         return lds_b6[((b * 3 + pl) * kB6M + row) * 2 + hf];
     };
     auto B_at = [&](int b, int pl, int col, int hf) -> uint4 & {
-        return lds_b6[2 * 3 * kB6M * 2 + ((b * 3 + pl) * kB6N + col) * 2 + hf];
+        return lds_b6[2 * 3 * kB6M * 2 + ((b * 3 + pl) * BN + col) * 2 + hf];
     };
     const int tid = threadIdx.x;
     const int wave = wave_id();
     const int lane = tid & 63;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int bj = tid & (kB6N - 1), bh = tid >> 8;        // X loader: column, k half
-    // W loader: pieces q0 = tid and q1 = tid + 512 of 768 (3 planes x 128 rows x 2 halves); the
-    // threads past 768 load piece q1 - 256 again and do not store it
-    const int q0pl = tid >> 8, q0row = (tid >> 1) & (kB6M - 1), q0hf = tid & 1;
-    const bool q1ok = tid + 512 < 3 * kB6M * 2;
-    const int q1 = q1ok ? tid + 512 : tid + 256;
-    const int q1pl = q1 >> 8, q1row = (q1 >> 1) & (kB6M - 1), q1hf = q1 & 1;
+    const int wm = wave / WN, wn = wave % WN;
+    const int bj = tid % BN, bh = tid / BN;                // X loader: column, k half
+    // W loader: pieces q = tid + NT u (u = 0, 1, 2) of 768 (3 planes x 128 rows x 2 halves); a
+    // thread past 768 loads a valid piece again and does not store it
+    int qpl[3], qrow[3], qhf[3];
+    bool qok[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int q0 = tid + NT * u;
+        qok[u] = q0 < NPIECE;
+        const int q = qok[u] ? q0 : tid;
+        qpl[u] = q >> 8;
+        qrow[u] = (q >> 1) & (kB6M - 1);
+        qhf[u] = q & 1;
+    }
     const int hl = lane >> 5;
     const int64_t S = kpad / kB6K;
     const int64_t plane_el = mpad * kpad;                  // bf16 elements per W plane
@@ -1358,7 +1373,7 @@ __global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
         const int64_t local = t >> 3;
         const int64_t jt = (local / n_it) * 8 + xcd;
         const int64_t it = local % n_it;
-        const int64_t i0 = it * kB6M, j0 = jt * kB6N;
+        const int64_t i0 = it * kB6M, j0 = jt * BN;
         if (j0 >= p) continue;                             // block-uniform
         floatx16 acc[2][2];
 #pragma unroll
@@ -1374,44 +1389,49 @@ __global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
         // number of loads in flight is the same on every path, so each split waits only for its
         // own loads.  Written as macros over named registers (no arrays behind a lambda's
         // reference capture, which hipcc put in scratch memory).
+        // Loads by buffer instructions: one SGPR resource + a per-lane 32-bit offset + a scalar
+        // offset each (no 64-bit address arithmetic per load), and a load past the resource's
+        // extent returns 0 -- X rows past n (the last K-step) and columns past p (their lanes'
+        // offset is pushed out of range) arrive as zeros, with no clamp, select or branch.  The
+        // launcher checks 16 rows x ld_x x 4 B < 2^31 and the split W < 2^31 B.
         const int64_t jx = j0 + bj;
         const bool jin = jx < p;
-        const int64_t jc = jin ? jx : p - 1;
-        const float *xcol = x + jc;
-        const uint16_t *wpa = wp + (int64_t)q0pl * plane_el + (i0 + q0row) * kpad + 8 * q0hf;
-        const uint16_t *wpb = wp + (int64_t)q1pl * plane_el + (i0 + q1row) * kpad + 8 * q1hf;
-        uint4 wa0, wb0, wa1, wb1;
+        const uint32_t xvoff = jin ? (uint32_t)jx * 4u : 0x80000000u;
+        const uint32_t rowb = (uint32_t)ld_x * 4u;
+        uint32_t wvoff[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+            wvoff[u] = (uint32_t)((((int64_t)qpl[u] * mpad + i0 + qrow[u]) * kpad + 8 * qhf[u]) * 2);
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint16_t *>(wp), (short)0, (int)(3 * plane_el * 2), 0x00020000);
+        uint4 wa0, wb0, wc0, wa1, wb1, wc1;
         float xv0[8], xv1[8];
-        // the X rows a wave loads (k0 + 8 bh + u) are wave-uniform: scalar row addresses, one
-        // 32-bit lane offset (the column)
         const int bhu = __builtin_amdgcn_readfirstlane(bh);
-        const uint32_t xoff = (uint32_t)jc * 4u;
 #define B6_FETCH(SET, S_)                                                                          \
         do {                                                                                       \
             const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
-            wa##SET = *reinterpret_cast<const uint4 *>(wpa + k0_);                                \
-            wb##SET = *reinterpret_cast<const uint4 *>(wpb + k0_);                                \
-            _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                        \
-                const int64_t k_ = k0_ + 8 * bhu + u;                                              \
-                const char *row_ = reinterpret_cast<const char *>(x + (k_ < n ? k_ : n - 1) * ld_x); \
-                xv##SET[u] = *reinterpret_cast<const float *>(row_ + xoff);                       \
-            }                                                                                      \
+            const int64_t ext_ = (n - k0_) * (int64_t)rowb;                                        \
+            const __amdgpu_buffer_rsrc_t xr_ = __builtin_amdgcn_make_buffer_rsrc(                  \
+                const_cast<float *>(x + k0_ * ld_x), (short)0,                                     \
+                (int)(ext_ < 0x7fffffffLL ? ext_ : 0x7fffffffLL), 0x00020000);                     \
+            const int wso_ = (int)(k0_ * 2);                                                       \
+            wa##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[0], wso_, 0)); \
+            wb##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[1], wso_, 0)); \
+            if (WN == 2) wc##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[2], wso_, 0)); \
+            _Pragma("unroll") for (int u = 0; u < 8; ++u)                                          \
+                xv##SET[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(       \
+                                 xr_, xvoff, (int)((8 * bhu + u) * rowb), 0));                     \
         } while (0)
-        // the split zeroes X past n rows or p columns (clamped loads above) by a bit mask, here,
-        // where the values are used -- not right behind the loads, which would wait for them
 #define B6_STASH(SET, BUF, S_)                                                                     \
         do {                                                                                       \
-            A_at(BUF, q0pl, q0row, q0hf ^ ((q0row >> 3) & 1)) = wa##SET;                           \
-            if (q1ok) A_at(BUF, q1pl, q1row, q1hf ^ ((q1row >> 3) & 1)) = wb##SET;                 \
-            float xm_[8];                                                                          \
-            _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                        \
-                const int64_t k_ = (S_) * kB6K + 8 * bhu + u;                                      \
-                const uint32_t m_ = (k_ < n && jin) ? 0xffffffffu : 0u;                             \
-                xm_[u] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, xv##SET[u]) & m_); \
-            }                                                                                      \
+            A_at(BUF, qpl[0], qrow[0], qhf[0] ^ ((qrow[0] >> 3) & 1)) = wa##SET;                   \
+            /* a thread without a second piece re-stores its first (q = tid): same data, same  \
+               place -- no branch in the step */                                                   \
+            A_at(BUF, qpl[1], qrow[1], qhf[1] ^ ((qrow[1] >> 3) & 1)) = wb##SET;                   \
+            if (WN == 2) A_at(BUF, qpl[2], qrow[2], qhf[2] ^ ((qrow[2] >> 3) & 1)) = wc##SET;      \
             uint32_t h_[4], m_[4], l_[4];                                                          \
             _Pragma("unroll") for (int u = 0; u < 4; ++u)                                          \
-                split3_pair(xm_[2 * u], xm_[2 * u + 1], h_[u], m_[u], l_[u]);                      \
+                split3_pair(xv##SET[2 * u], xv##SET[2 * u + 1], h_[u], m_[u], l_[u]);              \
             const int sh_ = bh ^ ((bj >> 3) & 1);                                                  \
             B_at(BUF, 0, bj, sh_) = make_uint4(h_[0], h_[1], h_[2], h_[3]);                        \
             B_at(BUF, 1, bj, sh_) = make_uint4(m_[0], m_[1], m_[2], m_[3]);                        \
@@ -1423,22 +1443,46 @@ __global__ __launch_bounds__(512, 1) void k_mix_dense_b6(
         do {                                                                                       \
             B6_FETCH(B, (S_) + 2);                                                                 \
             bf16x8v af_[2][3], bf_[2][3];                                                          \
-            _Pragma("unroll") for (int a = 0; a < 2; ++a) {                                        \
-                const int row_ = wm * 64 + a * 32 + (lane & 31);                                   \
-                _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                   \
-                    af_[a][pl] = __builtin_bit_cast(bf16x8v, A_at(B, pl, row_, hl ^ ((row_ >> 3) & 1))); \
-            }                                                                                      \
-            _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                        \
-                const int col_ = wn * 64 + c * 32 + (lane & 31);                                   \
-                _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                   \
-                    bf_[c][pl] = __builtin_bit_cast(bf16x8v, B_at(B, pl, col_, hl ^ ((col_ >> 3) & 1))); \
+            /* operand reads in the order the products use them: (A m, B m), (A l, B h), (A h, B l) */ \
+            _Pragma("unroll") for (int o = 0; o < 3; ++o) {                                        \
+                const int pa_ = o == 0 ? 1 : o == 1 ? 2 : 0, pb_ = o == 0 ? 1 : o == 1 ? 0 : 2;    \
+                _Pragma("unroll") for (int a = 0; a < 2; ++a) {                                    \
+                    const int row_ = wm * 64 + a * 32 + (lane & 31);                               \
+                    af_[a][pa_] = __builtin_bit_cast(bf16x8v, A_at(B, pa_, row_, hl ^ ((row_ >> 3) & 1))); \
+                }                                                                                  \
+                _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                    \
+                    const int col_ = wn * 64 + c * 32 + (lane & 31);                               \
+                    bf_[c][pb_] = __builtin_bit_cast(bf16x8v, B_at(B, pb_, col_, hl ^ ((col_ >> 3) & 1))); \
+                }                                                                                  \
             }                                                                                      \
             _Pragma("unroll") for (int e = 0; e < 6; ++e)                                          \
                 _Pragma("unroll") for (int a = 0; a < 2; ++a)                                      \
                     _Pragma("unroll") for (int c = 0; c < 2; ++c)                                  \
                         acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
                             af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
-            if ((S_) + 1 < S) B6_STASH(NB, NB, (S_) + 1);                                          \
+            /* unconditional (no branch between the MFMAs and the split): past the last K-step  \
+               it stores the clamped refetch into a buffer no step reads */                        \
+            B6_STASH(NB, NB, (S_) + 1);                                                            \
+            /* schedule: the loads; the operand reads in three slices of four (the products in  \
+               plane order mm, lh, hl, then mh, hm, hh need no new operands), MFMAs starting as   \
+               soon as the first slice lands; SCHED 0: the split beside the MFMAs, two VALU per    \
+               MFMA; SCHED 1: the split after them; the LDS writes last */                         \
+            __builtin_amdgcn_sched_group_barrier(0x020, 12, 0);                                    \
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                     \
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                                     \
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
+            if (SCHED == 0) {                                                                      \
+                _Pragma("unroll") for (int i_ = 0; i_ < 20; ++i_) {                                \
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                             \
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                             \
+                }                                                                                  \
+            } else {                                                                               \
+                __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);                                \
+                __builtin_amdgcn_sched_group_barrier(0x002, 80, 0);                                \
+            }                                                                                      \
+            __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);                                     \
             __syncthreads();                                                                       \
         } while (0)
         B6_FETCH(0, 0);
@@ -4163,15 +4207,28 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
         return set_error(NIIDMIX_EALIAS, "x and y overlap (mixing is out-of-place / Jacobi)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t mpad = (n + kB6M - 1) / kB6M * kB6M, kpad = (n + kB6K - 1) / kB6K * kB6K;
+    if (16 * ld_x * 4 >= (int64_t)0x7fffffffLL || 3 * mpad * kpad * 2 >= (int64_t)0x7fffffffLL)
+        return set_error(NIIDMIX_EUNSUPPORTED, "bf16x6 dense GEMM: 16 rows of ld_x %lld or the split W "
+                         "of n %lld exceed 2^31 B (use niidmix_mix_dense_f32)", (long long)ld_x, (long long)n);
     const int64_t n_it = mpad / kB6M;
-    const int64_t n_jt = (p + kB6N - 1) / kB6N;
-    const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
-    const size_t lds = (size_t)2 * 3 * (kB6M + kB6N) * 2 * sizeof(uint4);    // 72 KB
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return set_error(NIIDMIX_EHIP, "k_mix_dense_b6: %zu B of LDS refused", lds);
-    hipLaunchKernelGGL(k_mix_dense_b6, dim3((unsigned)grid_for(n_items)), dim3(512), lds, s, x, ld_x,
-                       y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val);
+    // block tile 128 x 256 (8 waves) by default; NIIDMIX_DENSE_B6_WN=2: 128 x 128 (4 waves, two
+    // blocks per CU; tuning A/B)
+    int wn = 4, sched = 0;
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_WN")) if (atoi(e) == 2) wn = 2;
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) if (atoi(e) == 1) sched = 1;
+#define NIIDMIX_B6(WN, SC) do { \
+        const int64_t n_jt = (p + 64 * WN - 1) / (64 * WN); \
+        const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8; \
+        const size_t lds = (size_t)2 * 3 * (kB6M + 64 * WN) * 2 * sizeof(uint4); \
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6<WN, SC>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+            return set_error(NIIDMIX_EHIP, "k_mix_dense_b6: %zu B of LDS refused", lds); \
+        hipLaunchKernelGGL((k_mix_dense_b6<WN, SC>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
+                           x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
+    } while (0)
+    if (wn == 2) { if (sched) NIIDMIX_B6(2, 1); else NIIDMIX_B6(2, 0); }
+    else { if (sched) NIIDMIX_B6(4, 1); else NIIDMIX_B6(4, 0); }
+#undef NIIDMIX_B6
     return check_launch("k_mix_dense_b6");
 }
 
