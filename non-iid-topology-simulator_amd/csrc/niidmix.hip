@@ -1467,22 +1467,24 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
                plane order mm, lh, hl, then mh, hm, hh need no new operands), MFMAs starting as   \
                soon as the first slice lands; SCHED 0: the split beside the MFMAs, two VALU per    \
                MFMA; SCHED 1: the split after them; the LDS writes last */                         \
+            if (SCHED < 2) {                                                                       \
             __builtin_amdgcn_sched_group_barrier(0x020, 12, 0);                                    \
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                     \
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
             __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                                     \
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                     \
+            }                                                                                      \
             if (SCHED == 0) {                                                                      \
                 _Pragma("unroll") for (int i_ = 0; i_ < 20; ++i_) {                                \
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                             \
                     __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                             \
                 }                                                                                  \
-            } else {                                                                               \
+            } else if (SCHED == 1) {                                                               \
                 __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);                                \
                 __builtin_amdgcn_sched_group_barrier(0x002, 80, 0);                                \
             }                                                                                      \
-            __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);                                     \
+            if (SCHED < 2) __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);                      \
             __syncthreads();                                                                       \
         } while (0)
         B6_FETCH(0, 0);
@@ -4213,9 +4215,12 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     const int64_t n_it = mpad / kB6M;
     // block tile 128 x 256 (8 waves) by default; NIIDMIX_DENSE_B6_WN=2: 128 x 128 (4 waves, two
     // blocks per CU; tuning A/B)
-    int wn = 4, sched = 0;
+    // schedule (tuning A/B, NIIDMIX_DENSE_B6_SCHED): 2 the compiler's (default: 11.2 ms on FC-1000
+    // at P = 2^20), 0 / 1 operand reads in three slices with the split beside / after the MFMAs
+    // (11.6-12.4 ms, profiles/r05/)
+    int wn = 4, sched = 2;
     if (const char *e = getenv("NIIDMIX_DENSE_B6_WN")) if (atoi(e) == 2) wn = 2;
-    if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) if (atoi(e) == 1) sched = 1;
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) { const int v = atoi(e); if (v == 0 || v == 1) sched = v; }
 #define NIIDMIX_B6(WN, SC) do { \
         const int64_t n_jt = (p + 64 * WN - 1) / (64 * WN); \
         const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8; \
@@ -4226,8 +4231,8 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
         hipLaunchKernelGGL((k_mix_dense_b6<WN, SC>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
-    if (wn == 2) { if (sched) NIIDMIX_B6(2, 1); else NIIDMIX_B6(2, 0); }
-    else { if (sched) NIIDMIX_B6(4, 1); else NIIDMIX_B6(4, 0); }
+    if (wn == 2) { if (sched == 2) NIIDMIX_B6(2, 2); else if (sched == 1) NIIDMIX_B6(2, 1); else NIIDMIX_B6(2, 0); }
+    else { if (sched == 2) NIIDMIX_B6(4, 2); else if (sched == 1) NIIDMIX_B6(4, 1); else NIIDMIX_B6(4, 0); }
 #undef NIIDMIX_B6
     return check_launch("k_mix_dense_b6");
 }
