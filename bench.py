@@ -326,6 +326,8 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
       cpu_only            the same rounds with the mixing removed (the CPU part of the round);
       row_streamed        the plugin's default: rows go H2D right after their optimizer.step(),
                           the mixed rows come back while the next round trains (deferred write-back);
+      row_streamed_paced  the same with the write-back paced (NIIDMIX_D2H_PACE=8: row blocks go D2H
+                          8 ahead of the training that needs them, not all at once);
       row_streamed_sync   the same, but next_step waits for every mixed row before returning;
       windowed            the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0);
       fused_*             the same two with --clique-gradient (gradient mean + SGD step + mixing
@@ -352,7 +354,7 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         def forward(self, x, params):
             return torch.nn.functional.log_softmax(self.fc(x), dim=1)
 
-    variants = ["cpu_only", "row_streamed", "row_streamed_sync", "windowed"]
+    variants = ["cpu_only", "row_streamed", "row_streamed_paced", "row_streamed_sync", "windowed"]
     if cliques:
         variants += ["fused_row_streamed", "fused_windowed"]
     orig, orig_rs = d_sgd.average, d_sgd._row_streamed
@@ -366,7 +368,8 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
                   "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": batch,
                                 "initial-averaging": False, "clique-gradient": fused,
                                 "unbiased-gradient": False, "mixing-mode": mode,
-                                "deferred-writeback": v in ("row_streamed", "fused_row_streamed")}}
+                                "deferred-writeback": v in ("row_streamed", "row_streamed_paced",
+                                                            "fused_row_streamed")}}
         torch.manual_seed(3)
         nodes = []
         for r in range(n):
@@ -381,6 +384,10 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             d_sgd._row_streamed = lambda p: False
         if v.endswith("windowed"):
             os.environ["NIIDMIX_RESIDENT"] = "0"          # read when the engine is built
+        # paced write-back (niidmix.slab.ResidentRound, NIIDMIX_D2H_PACE): 8 row blocks ahead
+        pace_env = os.environ.pop("NIIDMIX_D2H_PACE", None)
+        if v == "row_streamed_paced":
+            os.environ["NIIDMIX_D2H_PACE"] = "8"
         try:
             for key in ("wait_s", "enqueue_s"):
                 d_sgd.round_stats[key] = 0.0
@@ -396,6 +403,9 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
                 st["wait"] += d_sgd.round_stats["wait_s"]
         finally:
             d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+            os.environ.pop("NIIDMIX_D2H_PACE", None)
+            if pace_env is not None:
+                os.environ["NIIDMIX_D2H_PACE"] = pace_env
             if env_res is None:
                 os.environ.pop("NIIDMIX_RESIDENT", None)
             else:

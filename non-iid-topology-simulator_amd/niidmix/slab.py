@@ -408,6 +408,9 @@ class ResidentRound:
         self._count = [0] * self.nblk      # rows of each block made final this round
         self._sent = [False] * self.nblk
         self._done = None                  # per block: the D2H events of the last op
+        self._d2h_next = 0                 # row blocks whose D2H is enqueued (paced write-back)
+        self._d2h_outs = []
+        self._pace = 0
         # the device outputs (outs[0]: the mixed parameters) hold the models' current values: set
         # by mix(), cleared by begin() and by guarded writes (niidmix.guard); read by niidmix.logger
         self.fresh = False
@@ -440,6 +443,7 @@ class ResidentRound:
         self.fresh = False
         self._count = [0] * self.nblk
         self._sent = [False] * self.nblk
+        self._enqueue_d2h(self.nblk)               # a paced write-back: the rest now
         for pt in self.parts:
             pt["s_h2d"].wait_stream(pt["s_d2h"])   # the host rows come back before they go up
 
@@ -475,6 +479,7 @@ class ResidentRound:
         once."""
         t0 = time.perf_counter()
         delay = int(os.environ.get("NIIDMIX_D2H_DELAY_CYCLES", "0"))
+        self._enqueue_d2h(self.nblk)               # the previous round's paced write-back: all
         unsent = sum(1 for s in self._sent if not s)
         for b in range(self.nblk):
             if not self._sent[b]:
@@ -501,29 +506,53 @@ class ResidentRound:
                 if delay:                           # test knob: a late write-back (guard tests)
                     with torch.cuda.stream(sd):
                         torch.cuda._sleep(delay)
-                w = pt["w"]
-                for b in range(self.nblk):
-                    r0, rows = self._rows(b)
-                    for h, d in zip(self.hosts_out, pt["outs"]):
-                        _copy2d(h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4,
-                                d.data_ptr() + r0 * w * 4, w * 4, w * 4, rows, 1, sd)
-                    e = torch.cuda.Event()
-                    e.record(sd)
-                    done[b].append(e)
         self._done = done
+        self._d2h_next = 0
+        self._d2h_outs = list(self.hosts_out)
+        # paced write-back (NIIDMIX_D2H_PACE = L > 0): only the first L row blocks go D2H now; the
+        # rest follow as the next round's training reaches them (wait_row keeps L blocks ahead),
+        # spreading the 4.2 GB of a headline round over the training instead of one ~85 ms burst
+        # through the host's memory.  0 (default): every block now.
+        pace = int(os.environ.get("NIIDMIX_D2H_PACE", "0"))
+        self._enqueue_d2h(self.nblk if pace <= 0 else min(self.nblk, pace))
+        self._pace = pace
         self.fresh = True
         self.hosts = None                           # row_ready() is a no-op until begin()
         self._timing = (timing, t0, t_ev, unsent)
 
+    def _enqueue_d2h(self, upto):
+        """Enqueue the D2H of row blocks [_d2h_next, upto), one event per block and device."""
+        if self._done is None or upto <= self._d2h_next:
+            return
+        for pt in self.parts:
+            with torch.cuda.device(pt["dev"]):
+                sd = pt["s_d2h"]
+                w = pt["w"]
+                for b in range(self._d2h_next, upto):
+                    r0, rows = self._rows(b)
+                    for h, d in zip(self._d2h_outs, pt["outs"]):
+                        _copy2d(h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4,
+                                d.data_ptr() + r0 * w * 4, w * 4, w * 4, rows, 1, sd)
+                    e = torch.cuda.Event()
+                    e.record(sd)
+                    self._done[b].append(e)
+        self._d2h_next = upto
+
     def wait_row(self, i):
         """Block until row i's outputs are back in the host slabs."""
         if self._done is not None:
-            for e in self._done[i // self.block]:
+            b = i // self.block
+            if self._d2h_next <= b:
+                self._enqueue_d2h(min(self.nblk, b + max(self._pace, 1)))
+            elif self._pace > 0:
+                self._enqueue_d2h(min(self.nblk, b + self._pace))
+            for e in self._done[b]:
                 e.synchronize()
 
     def wait_all(self):
         if self._done is None:
             return
+        self._enqueue_d2h(self.nblk)
         for evs in self._done:
             for e in evs:
                 e.synchronize()

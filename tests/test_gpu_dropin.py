@@ -159,7 +159,7 @@ def test_training_rounds_match_reference_loop(gpu, oracle_mod):
         assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("resident", ["1", "0"])
+@pytest.mark.parametrize("resident", ["1", "0", "paced"])
 def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypatch):
     """The row-streamed round (rows go H2D right after their optimizer.step(), the mixed rows come
     back while the next round trains; niidmix.slab.ResidentRound) with deferred write-back, on a
@@ -169,6 +169,9 @@ def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypat
     where run.py's should_log (every 3rd step here) reads them; resident=0 runs the windowed
     engine (always synchronous)."""
     from niidmix import d_sgd
+    if resident == "paced":                               # write-back 2 row blocks ahead
+        monkeypatch.setenv("NIIDMIX_D2H_PACE", "2")
+        resident = "1"
     monkeypatch.setenv("NIIDMIX_RESIDENT", resident)
     monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")          # ragged last block (16 = 5 x 3 + 1)
     n = 16
