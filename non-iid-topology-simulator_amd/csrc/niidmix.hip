@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict_
 // fp32 GEMM's margin, at 16/6 = 2.7x the fp32 MFMA's rate.  Non-finite inputs make the splits NaN
 // (inf - inf) and the output non-finite, which the guard recomputes from the CSR (as k_mix_dense).
 //   W^T is split ONCE per topology (k_dense_split_w): wp[3][mpad][kpad] bf16, row i = output node,
-//   k contiguous, zero-padded (mpad = n rounded up to 128, kpad to 16).
+//   k contiguous, zero-padded (mpad = n rounded up to 256, kpad to 16).
 //   X is split as it is staged: LDS [plane][column][16 k] bf16, so a B operand's run of 8 k is one
 //   ds_read_b128; W tiles land in LDS [plane][row][16 k] the same way.
 // Block tile 128 rows x 256 columns, 8 waves (2 x 4), each 64 x 64 = 2 x 2 accumulators of
@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(256, OCC) void k_mix_dense(const float *__restrict_
 // maps (32x32x16 bf16): lane l holds A[l&31][8(l>>5) + 0..7] and B[8(l>>5) + 0..7][l&31]; C as
 // k_mix_dense.  The two 16-B halves of every 32-B LDS row swap places on alternate groups of 8
 // rows (half ^ (row >> 3 & 1)): the ds_read_b128 of 16 consecutive rows hit 16 distinct bank quads.
-constexpr int kB6M = 128, kB6K = 16;
+constexpr int kB6M = 256, kB6K = 16;   // W split padding: rows to 256, k to 16
 // the six split products (plane of A, plane of B), smallest first: mm, lh, hl, mh, hm, hh
 __device__ constexpr int kB6PA[6] = {1, 2, 0, 1, 0, 0}, kB6PB[6] = {1, 0, 2, 0, 1, 0};
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -1330,7 +1330,9 @@ __global__ __launch_bounds__(256) void k_dense_split_w(const float *__restrict__
 // SIMD, one barrier phase per CU), 2 -> 4-wave blocks of 128 x 128 (two blocks per CU, each with
 // its own barrier phase, so one block's split and barrier overlap the other's MFMAs; W is re-read
 // per 128 columns instead of 256)
-template <int WN, int SCHED>
+// ABL (tuning builds of the time split only, NIIDMIX_DENSE_B6_ABL; results are wrong): 1 no global
+// loads in the K loop, 2 no MFMAs, 3 no LDS operand reads
+template <int WN, int SCHED, int ABL = 0, int TM = 2>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
     int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
@@ -1338,14 +1340,17 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     const float *__restrict__ csr_val) {
     constexpr int NT = 128 * WN;                           // threads
     constexpr int BN = 64 * WN;                            // columns per block tile
-    constexpr int NPIECE = 3 * kB6M * 2;                   // 16-B W pieces per K-step (768)
+    constexpr int BM = 64 * TM;                            // rows per block tile (2 waves along M)
+    constexpr int NPIECE = 3 * BM * 2;                     // 16-B W pieces per K-step
+    constexpr int NPT = (NPIECE + NT - 1) / NT;            // pieces per thread (2 or 3)
+    static_assert(NPT <= 3, "W pieces per thread");
     extern __shared__ uint4 lds_b6[];
     // As[buf][plane][row][half] then Bs[buf][plane][col][half], 16 B each
     auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
-        return lds_b6[((b * 3 + pl) * kB6M + row) * 2 + hf];
+        return lds_b6[((b * 3 + pl) * BM + row) * 2 + hf];
     };
     auto B_at = [&](int b, int pl, int col, int hf) -> uint4 & {
-        return lds_b6[2 * 3 * kB6M * 2 + ((b * 3 + pl) * BN + col) * 2 + hf];
+        return lds_b6[2 * 3 * BM * 2 + ((b * 3 + pl) * BN + col) * 2 + hf];
     };
     const int tid = threadIdx.x;
     const int wave = wave_id();
@@ -1361,8 +1366,8 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
         const int q0 = tid + NT * u;
         qok[u] = q0 < NPIECE;
         const int q = qok[u] ? q0 : tid;
-        qpl[u] = q >> 8;
-        qrow[u] = (q >> 1) & (kB6M - 1);
+        qpl[u] = q / (2 * BM);
+        qrow[u] = (q >> 1) & (BM - 1);
         qhf[u] = q & 1;
     }
     const int hl = lane >> 5;
@@ -1373,11 +1378,11 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
         const int64_t local = t >> 3;
         const int64_t jt = (local / n_it) * 8 + xcd;
         const int64_t it = local % n_it;
-        const int64_t i0 = it * kB6M, j0 = jt * BN;
+        const int64_t i0 = it * BM, j0 = jt * BN;
         if (j0 >= p) continue;                             // block-uniform
-        floatx16 acc[2][2];
+        floatx16 acc[TM][2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -1415,12 +1420,17 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
                 const_cast<float *>(x + k0_ * ld_x), (short)0,                                     \
                 (int)(ext_ < 0x7fffffffLL ? ext_ : 0x7fffffffLL), 0x00020000);                     \
             const int wso_ = (int)(k0_ * 2);                                                       \
+            if (ABL != 1) {                                                                        \
             wa##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[0], wso_, 0)); \
             wb##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[1], wso_, 0)); \
-            if (WN == 2) wc##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[2], wso_, 0)); \
+            if (NPT == 3) wc##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[2], wso_, 0)); \
             _Pragma("unroll") for (int u = 0; u < 8; ++u)                                          \
                 xv##SET[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(       \
                                  xr_, xvoff, (int)((8 * bhu + u) * rowb), 0));                     \
+            } else {                                                                               \
+                wa##SET = make_uint4(k0_, 1, 2, 3); wb##SET = wa##SET; wc##SET = wa##SET;          \
+                _Pragma("unroll") for (int u = 0; u < 8; ++u) xv##SET[u] = (float)(k0_ + u);       \
+            }                                                                                      \
         } while (0)
 #define B6_STASH(SET, BUF, S_)                                                                     \
         do {                                                                                       \
@@ -1428,7 +1438,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
             /* a thread without a second piece re-stores its first (q = tid): same data, same  \
                place -- no branch in the step */                                                   \
             A_at(BUF, qpl[1], qrow[1], qhf[1] ^ ((qrow[1] >> 3) & 1)) = wb##SET;                   \
-            if (WN == 2) A_at(BUF, qpl[2], qrow[2], qhf[2] ^ ((qrow[2] >> 3) & 1)) = wc##SET;      \
+            if (NPT == 3) A_at(BUF, qpl[2], qrow[2], qhf[2] ^ ((qrow[2] >> 3) & 1)) = wc##SET;      \
             uint32_t h_[4], m_[4], l_[4];                                                          \
             _Pragma("unroll") for (int u = 0; u < 4; ++u)                                          \
                 split3_pair(xv##SET[2 * u], xv##SET[2 * u + 1], h_[u], m_[u], l_[u]);              \
@@ -1442,12 +1452,18 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
 #define B6_STEP(B, NB, S_)                                                                         \
         do {                                                                                       \
             B6_FETCH(B, (S_) + 2);                                                                 \
-            bf16x8v af_[2][3], bf_[2][3];                                                          \
+            bf16x8v af_[TM][3], bf_[2][3];                                                          \
             /* operand reads in the order the products use them: (A m, B m), (A l, B h), (A h, B l) */ \
+            if (ABL == 3) {                                                                        \
+                _Pragma("unroll") for (int q_ = 0; q_ < 3 * TM; ++q_)                              \
+                    af_[q_ / 3][q_ % 3] = __builtin_bit_cast(bf16x8v, make_uint4(lane, q_, 1, 2)); \
+                _Pragma("unroll") for (int q_ = 0; q_ < 6; ++q_)                                   \
+                    bf_[q_ / 3][q_ % 3] = __builtin_bit_cast(bf16x8v, make_uint4(q_, lane, 3, 4)); \
+            } else                                                                                 \
             _Pragma("unroll") for (int o = 0; o < 3; ++o) {                                        \
                 const int pa_ = o == 0 ? 1 : o == 1 ? 2 : 0, pb_ = o == 0 ? 1 : o == 1 ? 0 : 2;    \
-                _Pragma("unroll") for (int a = 0; a < 2; ++a) {                                    \
-                    const int row_ = wm * 64 + a * 32 + (lane & 31);                               \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a) {                                   \
+                    const int row_ = wm * 32 * TM + a * 32 + (lane & 31);                          \
                     af_[a][pa_] = __builtin_bit_cast(bf16x8v, A_at(B, pa_, row_, hl ^ ((row_ >> 3) & 1))); \
                 }                                                                                  \
                 _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                    \
@@ -1455,11 +1471,15 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
                     bf_[c][pb_] = __builtin_bit_cast(bf16x8v, B_at(B, pb_, col_, hl ^ ((col_ >> 3) & 1))); \
                 }                                                                                  \
             }                                                                                      \
+            if (ABL != 2)                                                                          \
             _Pragma("unroll") for (int e = 0; e < 6; ++e)                                          \
-                _Pragma("unroll") for (int a = 0; a < 2; ++a)                                      \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a)                                     \
                     _Pragma("unroll") for (int c = 0; c < 2; ++c)                                  \
                         acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
                             af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
+            else                                                                                   \
+                _Pragma("unroll") for (int q_ = 0; q_ < 6; ++q_)                                   \
+                    asm volatile("" :: "v"(af_[q_ % TM][q_ % 3]), "v"(bf_[q_ / 3][q_ % 3]));       \
             /* unconditional (no branch between the MFMAs and the split): past the last K-step  \
                it stores the clamped refetch into a buffer no step reads */                        \
             B6_STASH(NB, NB, (S_) + 1);                                                            \
@@ -1498,28 +1518,30 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
 #undef B6_STEP
 #undef B6_STASH
 #undef B6_FETCH
-        uint64_t bad = 0;                                  // this lane's non-finite outputs
+        uint64_t bad[2] = {0, 0};                          // this lane's non-finite outputs
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int64_t i = i0 + wm * 32 * TM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                     const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
                     if (i < n && j < p) {
                         if (__builtin_isfinite(acc[a][c][r])) __builtin_nontemporal_store(acc[a][c][r], y + i * ld_y + j);
-                        else bad |= 1ull << (a * 32 + c * 16 + r);
+                        else bad[a >> 1] |= 1ull << ((a & 1) * 32 + c * 16 + r);
                     }
                 }
-        while (bad) {                                      // non-finite guard (csr_refix1)
-            const int q = __builtin_ctzll(bad);
-            bad &= bad - 1;
-            const int a = q >> 5, c = (q >> 4) & 1, r = q & 15;
-            const int64_t i = i0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
-            __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
-        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            while (bad[h]) {                               // non-finite guard (csr_refix1)
+                const int q = __builtin_ctzll(bad[h]);
+                bad[h] &= bad[h] - 1;
+                const int a = 2 * h + (q >> 5), c = (q >> 4) & 1, r = q & 15;
+                const int64_t i = i0 + wm * 32 * TM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
+                __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
+            }
     }
 }
 
@@ -4212,7 +4234,10 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     if (16 * ld_x * 4 >= (int64_t)0x7fffffffLL || 3 * mpad * kpad * 2 >= (int64_t)0x7fffffffLL)
         return set_error(NIIDMIX_EUNSUPPORTED, "bf16x6 dense GEMM: 16 rows of ld_x %lld or the split W "
                          "of n %lld exceed 2^31 B (use niidmix_mix_dense_f32)", (long long)ld_x, (long long)n);
-    const int64_t n_it = mpad / kB6M;
+    // block tile 256 x 256 (8 waves of 128 x 64: X re-read by 4 row tiles instead of 8, 48 MFMAs
+    // per wave between barriers): 9.81-9.86 vs 11.20-11.30 ms for 128 x 256 on the same box
+    // (profiles/r05/dense_b6/); NIIDMIX_DENSE_B6_TM=2 selects the latter (with _WN / _SCHED: A/B)
+    const int tm = (getenv("NIIDMIX_DENSE_B6_TM") && atoi(getenv("NIIDMIX_DENSE_B6_TM")) == 2) ? 2 : 4;
     // block tile 128 x 256 (8 waves) by default; NIIDMIX_DENSE_B6_WN=2: 128 x 128 (4 waves, two
     // blocks per CU; tuning A/B)
     // schedule (tuning A/B, NIIDMIX_DENSE_B6_SCHED): 2 the compiler's (default: 11.2 ms on FC-1000
@@ -4221,19 +4246,28 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     int wn = 4, sched = 2;
     if (const char *e = getenv("NIIDMIX_DENSE_B6_WN")) if (atoi(e) == 2) wn = 2;
     if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) { const int v = atoi(e); if (v == 0 || v == 1) sched = v; }
-#define NIIDMIX_B6(WN, SC) do { \
+#define NIIDMIX_B6T(WN, SC, AB, TM) do { \
+        const int64_t n_it = mpad / (64 * TM); \
         const int64_t n_jt = (p + 64 * WN - 1) / (64 * WN); \
         const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8; \
-        const size_t lds = (size_t)2 * 3 * (kB6M + 64 * WN) * 2 * sizeof(uint4); \
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6<WN, SC>), \
+        const size_t lds = (size_t)2 * 3 * (64 * TM + 64 * WN) * 2 * sizeof(uint4); \
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6<WN, SC, AB, TM>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return set_error(NIIDMIX_EHIP, "k_mix_dense_b6: %zu B of LDS refused", lds); \
-        hipLaunchKernelGGL((k_mix_dense_b6<WN, SC>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
+        hipLaunchKernelGGL((k_mix_dense_b6<WN, SC, AB, TM>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
-    if (wn == 2) { if (sched == 2) NIIDMIX_B6(2, 2); else if (sched == 1) NIIDMIX_B6(2, 1); else NIIDMIX_B6(2, 0); }
-    else { if (sched == 2) NIIDMIX_B6(4, 2); else if (sched == 1) NIIDMIX_B6(4, 1); else NIIDMIX_B6(4, 0); }
+    int abl = 0;
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_ABL")) abl = atoi(e);
+#define NIIDMIX_B6(WN, SC, AB) NIIDMIX_B6T(WN, SC, AB, 2)
+    if (tm == 4 && abl == 0 && wn == 4 && sched == 2) NIIDMIX_B6T(4, 2, 0, 4);
+    else if (abl == 1) NIIDMIX_B6(4, 2, 1);
+    else if (abl == 2) NIIDMIX_B6(4, 2, 2);
+    else if (abl == 3) NIIDMIX_B6(4, 2, 3);
+    else if (wn == 2) { if (sched == 2) NIIDMIX_B6(2, 2, 0); else if (sched == 1) NIIDMIX_B6(2, 1, 0); else NIIDMIX_B6(2, 0, 0); }
+    else { if (sched == 2) NIIDMIX_B6(4, 2, 0); else if (sched == 1) NIIDMIX_B6(4, 1, 0); else NIIDMIX_B6(4, 0, 0); }
 #undef NIIDMIX_B6
+#undef NIIDMIX_B6T
     return check_launch("k_mix_dense_b6");
 }
 
