@@ -4261,9 +4261,9 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     if (const char *e = getenv("NIIDMIX_DENSE_B6_ABL")) abl = atoi(e);
 #define NIIDMIX_B6(WN, SC, AB) NIIDMIX_B6T(WN, SC, AB, 2)
     if (tm == 4 && abl == 0 && wn == 4 && sched == 2) NIIDMIX_B6T(4, 2, 0, 4);
-    else if (abl == 1) NIIDMIX_B6(4, 2, 1);
-    else if (abl == 2) NIIDMIX_B6(4, 2, 2);
-    else if (abl == 3) NIIDMIX_B6(4, 2, 3);
+    else if (abl == 1) NIIDMIX_B6T(4, 2, 1, 4);
+    else if (abl == 2) NIIDMIX_B6T(4, 2, 2, 4);
+    else if (abl == 3) NIIDMIX_B6T(4, 2, 3, 4);
     else if (wn == 2) { if (sched == 2) NIIDMIX_B6(2, 2, 0); else if (sched == 1) NIIDMIX_B6(2, 1, 0); else NIIDMIX_B6(2, 0, 0); }
     else { if (sched == 2) NIIDMIX_B6(4, 2, 0); else if (sched == 1) NIIDMIX_B6(4, 1, 0); else NIIDMIX_B6(4, 0, 0); }
 #undef NIIDMIX_B6

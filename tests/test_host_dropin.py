@@ -186,3 +186,36 @@ def test_read_guard_waits_for_own_row(monkeypatch):
     plain = [Net()]
     guard.install(plain, eng)
     assert type(plain[0]) is Net
+
+
+def test_logger_install_hooks_cpu(monkeypatch, tmp_path):
+    """niidmix.logger.install_hooks (called by niidmix.d_sgd.init) routes the reference driver's
+    Logger.log_consensus_distance always, and setup.model.average only with
+    log-global-model-accuracy; idempotent; NIIDMIX_GPU_LOGGER=0 / algorithm.gpu-logger false opt
+    out; nothing is touched when the reference's modules are not loaded."""
+    import types
+    from niidmix import logger as nl
+    monkeypatch.delitem(sys.modules, "simulate.logger", raising=False)
+    monkeypatch.delitem(sys.modules, "setup.model", raising=False)
+    assert nl.install_hooks({"logger": {"log-global-model-accuracy": True}}) == []
+    lg = types.ModuleType("simulate.logger")
+
+    class Logger:
+        def log_consensus_distance(self, state):
+            raise AssertionError("reference CPU version")
+    lg.Logger = Logger
+    sm = types.ModuleType("setup.model")
+    ref_avg = lambda models, weights=None: None   # noqa: E731
+    sm.average = ref_avg
+    monkeypatch.setitem(sys.modules, "simulate.logger", lg)
+    monkeypatch.setitem(sys.modules, "setup.model", sm)
+    monkeypatch.setenv("NIIDMIX_GPU_LOGGER", "0")
+    assert nl.install_hooks({"logger": {"log-global-model-accuracy": True}}) == []
+    monkeypatch.delenv("NIIDMIX_GPU_LOGGER")
+    assert nl.install_hooks({"logger": {}, "algorithm": {"gpu-logger": False}}) == []
+    assert nl.install_hooks({"logger": {}}) == ["simulate.logger.Logger.log_consensus_distance"]
+    assert Logger.log_consensus_distance is nl.log_consensus_distance and sm.average is ref_avg
+    done = nl.install_hooks({"logger": {"log-global-model-accuracy": True}})
+    assert done == ["simulate.logger.Logger.log_consensus_distance", "setup.model.average"]
+    assert sm.average is nl.average
+    assert nl.install_hooks({"logger": {"log-global-model-accuracy": True}}) == done
