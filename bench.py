@@ -324,6 +324,9 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
     round-robin (round k of every variant before round k + 1 of any, so that drifts of the host's
     speed hit all of them alike), each timed over `rounds` rounds after one warm-up round:
       cpu_only            the same rounds with the mixing removed (the CPU part of the round);
+      cpu_only_slab       the same with the parameters in the drop-in's pinned host slab (the
+                          baseline exposed_ms is taken against: that memory alone changes the
+                          CPU's training speed on some hosts);
       row_streamed        the plugin's default: rows go H2D right after their optimizer.step(),
                           the mixed rows come back while the next round trains (deferred write-back);
       row_streamed_paced  the same with the write-back paced (NIIDMIX_D2H_PACE=8: row blocks go D2H
@@ -332,7 +335,7 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
       windowed            the synchronous windowed round of rounds 1-3 (NIIDMIX_RESIDENT=0);
       fused_*             the same two with --clique-gradient (gradient mean + SGD step + mixing
                           on the device; parameter and gradient rows go up after each backward).
-    exposed_ms = median round - median cpu_only round (the mixing's cost the round still pays);
+    exposed_ms = median round - median cpu_only_slab round (the mixing's cost the round still pays);
     host_blocked_ms = the time next_step itself spent waiting for rows or enqueueing copies and
     kernels (d_sgd.round_stats), the part of exposed_ms the plugin controls."""
     from niidmix import d_sgd
@@ -354,7 +357,8 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         def forward(self, x, params):
             return torch.nn.functional.log_softmax(self.fc(x), dim=1)
 
-    variants = ["cpu_only", "row_streamed", "row_streamed_paced", "row_streamed_sync", "windowed"]
+    variants = ["cpu_only", "cpu_only_slab", "row_streamed", "row_streamed_paced",
+                "row_streamed_sync", "windowed"]
     if cliques:
         variants += ["fused_row_streamed", "fused_windowed"]
     orig, orig_rs = d_sgd.average, d_sgd._row_streamed
@@ -376,10 +380,16 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             mdl = Net()
             nodes.append({"rank": r, "epoch": 0, "train-set": data, "model": mdl,
                           "optimizer": d_sgd.optimizer(mdl, params)})
-        return {"params": params, "nodes": nodes, "ts": [], "blocked": 0.0, "wait": 0.0}
+        st = {"params": params, "nodes": nodes, "ts": [], "blocked": 0.0, "wait": 0.0}
+        if v == "cpu_only_slab":
+            # the CPU part with the models' parameters in the drop-in's pinned host slab (its
+            # memory trains at its own speed on some hosts), and no mixing
+            from niidmix.slab import NodeSlab
+            st["slab"] = NodeSlab([nd["model"] for nd in nodes])
+        return st
 
     def step(v, st, k):
-        if v == "cpu_only":
+        if v.startswith("cpu_only"):
             d_sgd.average = lambda nds, t, p: None
             d_sgd._row_streamed = lambda p: False
         if v.endswith("windowed"):
@@ -422,12 +432,17 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
            "batch": batch, "rounds_timed": rounds, "mode": mode, "threads": torch.get_num_threads(),
            "order": "round-robin over the variants"}
     base = float(np.median(sts["cpu_only"]["ts"]))
+    base_slab = float(np.median(sts["cpu_only_slab"]["ts"]))
+    res["exposed_vs"] = ("cpu_only_slab: the same CPU rounds with the parameters in the pinned "
+                         "slab and no mixing (exposed_ms_vs_plain_models: against models whose "
+                         "parameters are plain allocations)")
     for v in variants:
         st = sts[v]
         out = {"round_ms": round(float(np.median(st["ts"])) * 1e3, 1),
                "round_ms_min": round(min(st["ts"]) * 1e3, 1)}
-        if v != "cpu_only":
-            out["exposed_ms"] = round((float(np.median(st["ts"])) - base) * 1e3, 1)
+        if not v.startswith("cpu_only"):
+            out["exposed_ms"] = round((float(np.median(st["ts"])) - base_slab) * 1e3, 1)
+            out["exposed_ms_vs_plain_models"] = round((float(np.median(st["ts"])) - base) * 1e3, 1)
             out["host_blocked_ms"] = round(st["blocked"] / rounds * 1e3, 2)
             out["host_wait_ms"] = round(st["wait"] / rounds * 1e3, 2)
         res[v] = out

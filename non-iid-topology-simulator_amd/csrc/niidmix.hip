@@ -1330,8 +1330,8 @@ __global__ __launch_bounds__(256) void k_dense_split_w(const float *__restrict__
 // SIMD, one barrier phase per CU), 2 -> 4-wave blocks of 128 x 128 (two blocks per CU, each with
 // its own barrier phase, so one block's split and barrier overlap the other's MFMAs; W is re-read
 // per 128 columns instead of 256)
-// ABL (tuning builds of the time split only, NIIDMIX_DENSE_B6_ABL; results are wrong): 1 no global
-// loads in the K loop, 2 no MFMAs, 3 no LDS operand reads
+// ABL (time-split builds only: -DNIIDMIX_ABLATIONS, NIIDMIX_DENSE_B6_ABL; results are wrong): 1 no
+// global loads in the K loop, 2 no MFMAs, 3 no LDS operand reads
 template <int WN, int SCHED, int ABL = 0, int TM = 2>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
@@ -1452,6 +1452,9 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
 #define B6_STEP(B, NB, S_)                                                                         \
         do {                                                                                       \
             B6_FETCH(B, (S_) + 2);                                                                 \
+            /* SCHED 3: the loads stay at the top of the step (the compiler's schedule sinks them  \
+               below the MFMAs, and the next step's split waits for them) */                       \
+            if (SCHED == 3) __builtin_amdgcn_sched_barrier(0);                                     \
             bf16x8v af_[TM][3], bf_[2][3];                                                          \
             /* operand reads in the order the products use them: (A m, B m), (A l, B h), (A h, B l) */ \
             if (ABL == 3) {                                                                        \
@@ -1511,10 +1514,16 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
         B6_STASH(0, 0, 0);
         B6_FETCH(1, 1);
         __syncthreads();
-        for (int64_t s = 0; s < S; s += 2) {
+        // the loop body is both steps with no branch between them and an odd last step peeled off:
+        // with `if (s + 1 < S)` around the second step, the path that skips it reached the loop
+        // header with the first step's loads in flight, and the compiler waited for every load
+        // (vmcnt(0)) at the top of each iteration
+        int64_t s = 0;
+        for (; s + 1 < S; s += 2) {
             B6_STEP(0, 1, s);
-            if (s + 1 < S) B6_STEP(1, 0, s + 1);
+            B6_STEP(1, 0, s + 1);
         }
+        if (s < S) B6_STEP(0, 1, s);
 #undef B6_STEP
 #undef B6_STASH
 #undef B6_FETCH
@@ -4238,14 +4247,15 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     // per wave between barriers): 9.81-9.86 vs 11.20-11.30 ms for 128 x 256 on the same box
     // (profiles/r05/dense_b6/); NIIDMIX_DENSE_B6_TM=2 selects the latter (with _WN / _SCHED: A/B)
     const int tm = (getenv("NIIDMIX_DENSE_B6_TM") && atoi(getenv("NIIDMIX_DENSE_B6_TM")) == 2) ? 2 : 4;
-    // block tile 128 x 256 (8 waves) by default; NIIDMIX_DENSE_B6_WN=2: 128 x 128 (4 waves, two
-    // blocks per CU; tuning A/B)
-    // schedule (tuning A/B, NIIDMIX_DENSE_B6_SCHED): 2 the compiler's (default: 11.2 ms on FC-1000
-    // at P = 2^20), 0 / 1 operand reads in three slices with the split beside / after the MFMAs
-    // (11.6-12.4 ms, profiles/r05/)
-    int wn = 4, sched = 2;
+    // tuning A/B of the 128 x 256 tile (TM 2): NIIDMIX_DENSE_B6_WN=2 128 x 128 (4 waves, two blocks
+    // per CU); NIIDMIX_DENSE_B6_SCHED 2 the compiler's schedule (11.2 ms on FC-1000 at P = 2^20),
+    // 0 / 1 operand reads in three slices with the split beside / after the MFMAs (11.6-12.4 ms,
+    // profiles/r05/dense_b6/)
+    // SCHED 3 (loads pinned at the top of each K-step) by default on the 256 x 256 tile: 9.70-9.75
+    // vs 9.80-9.84 ms for the compiler's schedule (2), same box, interleaved (profiles/r05/dense_b6/)
+    int wn = 4, sched = tm == 4 ? 3 : 2;
     if (const char *e = getenv("NIIDMIX_DENSE_B6_WN")) if (atoi(e) == 2) wn = 2;
-    if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) { const int v = atoi(e); if (v == 0 || v == 1) sched = v; }
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_SCHED")) { const int v = atoi(e); if (v >= 0 && v <= 3) sched = v; }
 #define NIIDMIX_B6T(WN, SC, AB, TM) do { \
         const int64_t n_it = mpad / (64 * TM); \
         const int64_t n_jt = (p + 64 * WN - 1) / (64 * WN); \
@@ -4258,14 +4268,20 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
     int abl = 0;
+#ifdef NIIDMIX_ABLATIONS
+    // time-split builds only (wrong results by construction; never in the shipped library)
     if (const char *e = getenv("NIIDMIX_DENSE_B6_ABL")) abl = atoi(e);
+#endif
 #define NIIDMIX_B6(WN, SC, AB) NIIDMIX_B6T(WN, SC, AB, 2)
     if (tm == 4 && abl == 0 && wn == 4 && sched == 2) NIIDMIX_B6T(4, 2, 0, 4);
+    else if (tm == 4 && abl == 0 && wn == 4 && sched == 3) NIIDMIX_B6T(4, 3, 0, 4);
+#ifdef NIIDMIX_ABLATIONS
     else if (abl == 1) NIIDMIX_B6T(4, 2, 1, 4);
     else if (abl == 2) NIIDMIX_B6T(4, 2, 2, 4);
     else if (abl == 3) NIIDMIX_B6T(4, 2, 3, 4);
-    else if (wn == 2) { if (sched == 2) NIIDMIX_B6(2, 2, 0); else if (sched == 1) NIIDMIX_B6(2, 1, 0); else NIIDMIX_B6(2, 0, 0); }
-    else { if (sched == 2) NIIDMIX_B6(4, 2, 0); else if (sched == 1) NIIDMIX_B6(4, 1, 0); else NIIDMIX_B6(4, 0, 0); }
+#endif
+    else if (wn == 2) { if (sched >= 2) NIIDMIX_B6(2, 2, 0); else if (sched == 1) NIIDMIX_B6(2, 1, 0); else NIIDMIX_B6(2, 0, 0); }
+    else { if (sched >= 2) NIIDMIX_B6(4, 2, 0); else if (sched == 1) NIIDMIX_B6(4, 1, 0); else NIIDMIX_B6(4, 0, 0); }
 #undef NIIDMIX_B6
 #undef NIIDMIX_B6T
     return check_launch("k_mix_dense_b6");
