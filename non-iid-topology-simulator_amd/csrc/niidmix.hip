@@ -2209,6 +2209,23 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 #define NIIDMIX_UPD_FAST13(XD) NIIDMIX_UPD_FAST12(XD) NIIDMIX_FMA1("v[56:57]", XD)
 #define NIIDMIX_UPD_FAST14(XD) NIIDMIX_UPD_FAST13(XD) NIIDMIX_FMA1("v[58:59]", XD)
 #define NIIDMIX_UPD_FAST15(XD) NIIDMIX_UPD_FAST14(XD) NIIDMIX_FMA1("v[60:61]", XD)
+#if NIIDMIX_TLDS_SPLIT == 6 || NIIDMIX_TLDS_SPLIT == 7
+// time-split builds only (wrong results): 6 no per-position weight select and skip test, 7 no skip
+// test (the cost of the per-position scalar bookkeeping a pre-split run table would remove)
+#define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
+    "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
+    NIIDMIX_SEG_WSEL                                                                                 \
+    "s_waitcnt lgkmcnt(2)\n\t" UPD(XD)                                                               \
+    "\n.Lseg_back" K "_%=:\n\t"                                                                     \
+    "s_add_u32 s47, s47, 1\n\t"                                                                      \
+    "s_cmp_ge_u32 s47, s38\n\t"                                                                      \
+    "s_cbranch_scc1 .Lw_next_%=\n\t"
+#if NIIDMIX_TLDS_SPLIT == 7
+#define NIIDMIX_SEG_WSEL "s_bitcmp1_b32 s42, s47\n\t" "s_cselect_b32 s44, %[w1], %[w0]\n\t"
+#else
+#define NIIDMIX_SEG_WSEL
+#endif
+#else
 #define NIIDMIX_SEG_POS(XD, XP, OFF, K, UPD)                                                         \
     "ds_read_b64 " XP ", %[va] offset:%[" OFF "]\n\t"                                                \
     "s_bitcmp1_b32 s42, s47\n\t"                                                                     \
@@ -2220,6 +2237,7 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
     "s_add_u32 s47, s47, 1\n\t"                                                                      \
     "s_cmp_ge_u32 s47, s38\n\t"                                                                      \
     "s_cbranch_scc1 .Lw_next_%=\n\t"
+#endif
 #define NIIDMIX_SEG_SKIPBLK(XD, K, UPD)                                                              \
     "\n.Lseg_skip" K "_%=:\n\t"                                                                     \
     "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
