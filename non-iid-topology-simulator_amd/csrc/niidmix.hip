@@ -1331,7 +1331,8 @@ __global__ __launch_bounds__(256) void k_dense_split_w(const float *__restrict__
 // its own barrier phase, so one block's split and barrier overlap the other's MFMAs; W is re-read
 // per 128 columns instead of 256)
 // ABL (time-split builds only: -DNIIDMIX_ABLATIONS, NIIDMIX_DENSE_B6_ABL; results are wrong): 1 no
-// global loads in the K loop, 2 no MFMAs, 3 no LDS operand reads
+// global loads in the K loop, 2 no MFMAs, 3 no LDS operand reads, 4 X as if pre-split (three
+// 16-B pieces loaded and stored per thread and K-step, no split)
 template <int WN, int SCHED, int ABL = 0, int TM = 2>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
@@ -1410,6 +1411,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
         const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint16_t *>(wp), (short)0, (int)(3 * plane_el * 2), 0x00020000);
         uint4 wa0, wb0, wc0, wa1, wb1, wc1;
+        uint4 xq0[3], xq1[3];                              // ABL 4 only (pre-split X pieces)
         float xv0[8], xv1[8];
         const int bhu = __builtin_amdgcn_readfirstlane(bh);
 #define B6_FETCH(SET, S_)                                                                          \
@@ -1424,6 +1426,11 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
             wa##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[0], wso_, 0)); \
             wb##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[1], wso_, 0)); \
             if (NPT == 3) wc##SET = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[2], wso_, 0)); \
+            if (ABL == 4) {                                                                        \
+                _Pragma("unroll") for (int u = 0; u < 3; ++u)                                      \
+                    xq##SET[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(  \
+                        wrs, wvoff[u] ^ 0x400u, wso_, 0));                                         \
+            } else                                                                                 \
             _Pragma("unroll") for (int u = 0; u < 8; ++u)                                          \
                 xv##SET[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(       \
                                  xr_, xvoff, (int)((8 * bhu + u) * rowb), 0));                     \
@@ -1439,13 +1446,17 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
                place -- no branch in the step */                                                   \
             A_at(BUF, qpl[1], qrow[1], qhf[1] ^ ((qrow[1] >> 3) & 1)) = wb##SET;                   \
             if (NPT == 3) A_at(BUF, qpl[2], qrow[2], qhf[2] ^ ((qrow[2] >> 3) & 1)) = wc##SET;      \
+            const int sh_ = bh ^ ((bj >> 3) & 1);                                                  \
+            if (ABL == 4) {                                                                        \
+                _Pragma("unroll") for (int u = 0; u < 3; ++u) B_at(BUF, u, bj, sh_) = xq##SET[u];  \
+            } else {                                                                               \
             uint32_t h_[4], m_[4], l_[4];                                                          \
             _Pragma("unroll") for (int u = 0; u < 4; ++u)                                          \
                 split3_pair(xv##SET[2 * u], xv##SET[2 * u + 1], h_[u], m_[u], l_[u]);              \
-            const int sh_ = bh ^ ((bj >> 3) & 1);                                                  \
             B_at(BUF, 0, bj, sh_) = make_uint4(h_[0], h_[1], h_[2], h_[3]);                        \
             B_at(BUF, 1, bj, sh_) = make_uint4(m_[0], m_[1], m_[2], m_[3]);                        \
             B_at(BUF, 2, bj, sh_) = make_uint4(l_[0], l_[1], l_[2], l_[3]);                        \
+            }                                                                                      \
         } while (0)
         // K-step s on LDS buffer B = s & 1: issue the loads of s + 2 (register set B), read the
         // operands, run the MFMAs, split s + 1 (set B ^ 1) into buffer B ^ 1, barrier
@@ -4297,6 +4308,8 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
     else if (abl == 1) NIIDMIX_B6T(4, 2, 1, 4);
     else if (abl == 2) NIIDMIX_B6T(4, 2, 2, 4);
     else if (abl == 3) NIIDMIX_B6T(4, 2, 3, 4);
+    else if (abl == 4) NIIDMIX_B6T(4, 3, 4, 4);
+    else if (abl == 5) NIIDMIX_B6T(4, 3, 0, 4);
 #endif
     else if (wn == 2) { if (sched >= 2) NIIDMIX_B6(2, 2, 0); else if (sched == 1) NIIDMIX_B6(2, 1, 0); else NIIDMIX_B6(2, 0, 0); }
     else { if (sched >= 2) NIIDMIX_B6(4, 2, 0); else if (sched == 1) NIIDMIX_B6(4, 1, 0); else NIIDMIX_B6(4, 0, 0); }
