@@ -1565,6 +1565,160 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void k_mix_dense_b6(
     }
 }
 
+// The same GEMM with ONE wave per SIMD (round 5, tuning A/B: NIIDMIX_DENSE_B6_W1=1): a 256 x 256
+// block tile of 4 waves of 128 x 128 (4 x 4 accumulators = 256 registers, which the compiler puts
+// in AGPRs: a wave of a one-wave-per-SIMD kernel has 256 VGPRs + 256 AGPRs), 96 MFMAs per wave per
+// K-step -- twice the two-wave kernel's per barrier -- while the split, the LDS writes and the next
+// loads issue between them.  Per thread and K-step: 6 W pieces and one column's 16 X values.
+// Products, K order and MFMA per output element are those of k_mix_dense_b6: bit-identical results.
+__global__ __launch_bounds__(256, 1) void k_mix_dense_b6w(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
+    int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
+    int64_t n_items, const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
+    const float *__restrict__ csr_val) {
+    constexpr int NT = 256, BM = 256, BN = 256, TM = 4, TN = 4;
+    constexpr int NPT = 3 * BM * 2 / NT;                   // W pieces per thread: 6
+    extern __shared__ uint4 lds_b6[];
+    auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
+        return lds_b6[((b * 3 + pl) * BM + row) * 2 + hf];
+    };
+    auto B_at = [&](int b, int pl, int col, int hf) -> uint4 & {
+        return lds_b6[2 * 3 * BM * 2 + ((b * 3 + pl) * BN + col) * 2 + hf];
+    };
+    const int tid = threadIdx.x;
+    const int wave = wave_id();
+    const int lane = tid & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int bj = tid;                                    // X loader: one column, all 16 k
+    int qpl[NPT], qrow[NPT], qhf[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+        const int q = tid + NT * u;
+        qpl[u] = q / (2 * BM);
+        qrow[u] = (q >> 1) & (BM - 1);
+        qhf[u] = q & 1;
+    }
+    const int hl = lane >> 5;
+    const int64_t S = kpad / kB6K;
+    const int64_t plane_el = mpad * kpad;
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t jt = (local / n_it) * 8 + xcd;
+        const int64_t it = local % n_it;
+        const int64_t i0 = it * BM, j0 = jt * BN;
+        if (j0 >= p) continue;                             // block-uniform
+        floatx16 acc[TM][TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int c = 0; c < TN; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+        const int64_t jx = j0 + bj;
+        const uint32_t xvoff = jx < p ? (uint32_t)jx * 4u : 0x80000000u;
+        const uint32_t rowb = (uint32_t)ld_x * 4u;
+        uint32_t wvoff[NPT];
+#pragma unroll
+        for (int u = 0; u < NPT; ++u)
+            wvoff[u] = (uint32_t)((((int64_t)qpl[u] * mpad + i0 + qrow[u]) * kpad + 8 * qhf[u]) * 2);
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint16_t *>(wp), (short)0, (int)(3 * plane_el * 2), 0x00020000);
+        uint4 wq0[NPT], wq1[NPT];
+        float xv0[16], xv1[16];
+#define B6W_FETCH(SET, S_)                                                                         \
+        do {                                                                                       \
+            const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
+            const int64_t ext_ = (n - k0_) * (int64_t)rowb;                                        \
+            const __amdgpu_buffer_rsrc_t xr_ = __builtin_amdgcn_make_buffer_rsrc(                  \
+                const_cast<float *>(x + k0_ * ld_x), (short)0,                                     \
+                (int)(ext_ < 0x7fffffffLL ? ext_ : 0x7fffffffLL), 0x00020000);                     \
+            const int wso_ = (int)(k0_ * 2);                                                       \
+            _Pragma("unroll") for (int u = 0; u < NPT; ++u)                                        \
+                wq##SET[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(      \
+                                 wrs, wvoff[u], wso_, 0));                                         \
+            _Pragma("unroll") for (int u = 0; u < 16; ++u)                                         \
+                xv##SET[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(       \
+                                 xr_, xvoff, (int)(u * rowb), 0));                                 \
+        } while (0)
+#define B6W_STASH(SET, BUF)                                                                        \
+        do {                                                                                       \
+            _Pragma("unroll") for (int u = 0; u < NPT; ++u)                                        \
+                A_at(BUF, qpl[u], qrow[u], qhf[u] ^ ((qrow[u] >> 3) & 1)) = wq##SET[u];            \
+            _Pragma("unroll") for (int hf = 0; hf < 2; ++hf) {                                     \
+                uint32_t h_[4], m_[4], l_[4];                                                      \
+                _Pragma("unroll") for (int u = 0; u < 4; ++u)                                      \
+                    split3_pair(xv##SET[8 * hf + 2 * u], xv##SET[8 * hf + 2 * u + 1], h_[u], m_[u], l_[u]); \
+                const int sh_ = hf ^ ((bj >> 3) & 1);                                              \
+                B_at(BUF, 0, bj, sh_) = make_uint4(h_[0], h_[1], h_[2], h_[3]);                    \
+                B_at(BUF, 1, bj, sh_) = make_uint4(m_[0], m_[1], m_[2], m_[3]);                    \
+                B_at(BUF, 2, bj, sh_) = make_uint4(l_[0], l_[1], l_[2], l_[3]);                    \
+            }                                                                                      \
+        } while (0)
+#define B6W_STEP(B, NB, S_)                                                                        \
+        do {                                                                                       \
+            B6W_FETCH(B, (S_) + 2);                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            bf16x8v af_[TM][3], bf_[TN][3];                                                         \
+            _Pragma("unroll") for (int o = 0; o < 3; ++o) {                                        \
+                const int pa_ = o == 0 ? 1 : o == 1 ? 2 : 0, pb_ = o == 0 ? 1 : o == 1 ? 0 : 2;    \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a) {                                   \
+                    const int row_ = wm * 128 + a * 32 + (lane & 31);                              \
+                    af_[a][pa_] = __builtin_bit_cast(bf16x8v, A_at(B, pa_, row_, hl ^ ((row_ >> 3) & 1))); \
+                }                                                                                  \
+                _Pragma("unroll") for (int c = 0; c < TN; ++c) {                                   \
+                    const int col_ = wn * 128 + c * 32 + (lane & 31);                              \
+                    bf_[c][pb_] = __builtin_bit_cast(bf16x8v, B_at(B, pb_, col_, hl ^ ((col_ >> 3) & 1))); \
+                }                                                                                  \
+            }                                                                                      \
+            _Pragma("unroll") for (int e = 0; e < 6; ++e)                                          \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a)                                     \
+                    _Pragma("unroll") for (int c = 0; c < TN; ++c)                                 \
+                        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
+                            af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
+            B6W_STASH(NB, NB);                                                                     \
+            __syncthreads();                                                                       \
+        } while (0)
+        B6W_FETCH(0, 0);
+        B6W_STASH(0, 0);
+        B6W_FETCH(1, 1);
+        __syncthreads();
+        int64_t s = 0;
+        for (; s + 1 < S; s += 2) {
+            B6W_STEP(0, 1, s);
+            B6W_STEP(1, 0, s + 1);
+        }
+        if (s < S) B6W_STEP(0, 1, s);
+#undef B6W_STEP
+#undef B6W_STASH
+#undef B6W_FETCH
+        uint64_t bad[4] = {0, 0, 0, 0};                    // this lane's non-finite outputs
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int c = 0; c < TN; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t i = i0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int64_t j = j0 + wn * 128 + c * 32 + (lane & 31);
+                    if (i < n && j < p) {
+                        if (__builtin_isfinite(acc[a][c][r])) __builtin_nontemporal_store(acc[a][c][r], y + i * ld_y + j);
+                        else bad[a] |= 1ull << (c * 16 + r);
+                    }
+                }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+            while (bad[a]) {                               // non-finite guard (csr_refix1)
+                const int q = __builtin_ctzll(bad[a]);
+                bad[a] &= bad[a] - 1;
+                const int c = q >> 4, r = q & 15;
+                const int64_t i = i0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int64_t j = j0 + wn * 128 + c * 32 + (lane & 31);
+                __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
+            }
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // Clique-factored mixing for BIG cliques (> 256 members, e.g. a fully-connected topology with MH
 // weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), WAVES waves, lane =
@@ -4296,6 +4450,18 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
         hipLaunchKernelGGL((k_mix_dense_b6<WN, SC, AB, TM>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
+    // one wave per SIMD (k_mix_dense_b6w, 256 x 256 tile of 4 waves of 128 x 128): tuning A/B
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_W1")) if (atoi(e) == 1) {
+        const int64_t n_it = mpad / 256, n_jt = (p + 255) / 256;
+        const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8;
+        const size_t lds = (size_t)2 * 3 * (256 + 256) * 2 * sizeof(uint4);
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6w),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return set_error(NIIDMIX_EHIP, "k_mix_dense_b6w: %zu B of LDS refused", lds);
+        hipLaunchKernelGGL(k_mix_dense_b6w, dim3((unsigned)grid_for(n_items)), dim3(256), lds, s,
+                           x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val);
+        return check_launch("k_mix_dense_b6w");
+    }
     int abl = 0;
 #ifdef NIIDMIX_ABLATIONS
     // time-split builds only (wrong results by construction; never in the shipped library)

@@ -758,6 +758,26 @@ def test_dense_b6_split_gemm(n, p, gpu, oracle_mod):
     assert worst["dense"] <= 4 * max(worst["dense-f32"], 1e-7), worst
 
 
+@pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (257, 1030), (300, 70000)])
+def test_dense_b6_one_wave_per_simd_bitwise(n, p, gpu, monkeypatch):
+    """The one-wave-per-SIMD bf16x6 kernel (k_mix_dense_b6w, 4 waves of 128 x 128) and the
+    two-wave kernel (8 waves of 128 x 64) run the same products in the same K order through the
+    same MFMA per output element: their outputs are bit-identical, non-finite guard included."""
+    ops = _ops()
+    rng = np.random.default_rng(7 * n + p)
+    w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)
+    w /= w.sum(0, keepdims=True)
+    m = ops.Mixer(csr=ops.csr_from_numpy(*_dense_csr(w)), device=gpu)
+    xn = rng.standard_normal((n, p)).astype(np.float32)
+    xn[n // 2, p // 3] = np.inf                       # a non-finite input: its column is recomputed
+    x = torch.from_numpy(xn).to(gpu)
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("NIIDMIX_DENSE_B6_W1", v)
+        out[v] = m(x, kernel="dense").cpu().numpy()
+    assert np.array_equal(out["0"].view(np.uint32), out["1"].view(np.uint32))
+
+
 def _dense_csr(w):
     """CSR of W^T rows (self first) of a dense [N, N] W (every entry an edge)."""
     n = w.shape[0]
