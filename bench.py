@@ -96,6 +96,8 @@ def parse():
                     help="also time the drop-in's WHOLE round (d_sgd.next_step: CPU training of every "
                          "node, optimizer steps, mixing) with and without the mixing, and report the "
                          "mixing's exposed cost per round (row-streamed / windowed)")
+    ap.add_argument("--e2e-threads", type=int, default=0,
+                    help="--e2e-step: torch CPU threads for the training (default: torch's own count)")
     ap.add_argument("--layout", default="blocked", choices=["blocked", "blocked-rank", "rowmajor"],
                     help="single GPU, clique kernel: device-resident slabs column-blocked [P/B, N, B] "
                          "with clique-contiguous rows and B per plan (Mixer.device_layout, default), "
@@ -1153,6 +1155,8 @@ def main():
             xa = xb = None                              # noqa: F841 (free the device slabs)
             torch.cuda.empty_cache()
             e2e = dict(e2e or {})
+            if args.e2e_threads > 0:
+                torch.set_num_threads(args.e2e_threads)
             e2e["next_step"] = e2e_next_step(csr, cliques, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config != "dcliques10000":
