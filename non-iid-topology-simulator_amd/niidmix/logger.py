@@ -73,10 +73,12 @@ def _stats_resident(rr):
             mean = torch.empty(x.shape[1], dtype=torch.float32, device=pt["dev"])
             dist2 = torch.empty(x.shape[0], dtype=torch.float64, device=pt["dev"])
             ops.mean_rows(x, mean, dist2, ops.EXACT)
-            d2.append(dist2)
-            nrm.append(torch.sum(mean.double() ** 2))
-    dist2 = sum(t.cpu() for t in d2)
-    return dist2.numpy(), float(sum(float(v.cpu()) for v in nrm))
+            sq = torch.sum(mean.double() ** 2)
+            # read back on the same (non-blocking) stream: a copy on the default stream would not
+            # wait for the statistics
+            d2.append(dist2.cpu())
+            nrm.append(float(sq.cpu()))
+    return sum(d2).numpy(), float(sum(nrm))
 
 
 def _stats_host_slab(host, device, window=1 << 18):

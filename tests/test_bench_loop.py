@@ -249,3 +249,15 @@ def test_node_leg_intercliques():
     assert bench.node_leg_intercliques("ring, smallworld", "x") == ["ring", "smallworld"]
     with pytest.raises(SystemExit):
         bench.node_leg_intercliques("mesh", "x")
+
+
+@pytest.mark.gpu
+def test_world_identity_on_the_gpu():
+    """bench.world_identity on a real GPU (the N > 1 line's config.world): the device's UUID and
+    PCI address, and the RCCL version torch links, are readable on this image."""
+    import bench
+    w = bench.world_identity(torch.device("cuda:0"), None, 1, "nccl")
+    assert w["backend"] == "nccl" and w["world_size"] == 1 and w["distinct_devices"] == 1
+    d = w["devices"][0]
+    assert d["uuid"] and d["pci"] and d["name"]
+    assert w["rccl_version"] and not str(w["rccl_version"]).startswith("unavailable"), w
