@@ -5,6 +5,8 @@
 //   mode 0: 8 independent v_mfma_f32_16x16x4_f32 per iteration (MFMA only)
 //   mode 1: NV independent v_pk_add_f32 per iteration (VALU only)
 //   mode 2: both, NV / 8 pk_adds after each MFMA (one instruction stream)
+//   mode 3: NV independent v_add_f32 per iteration (unpacked VALU only)
+//   mode 4: 8 MFMAs with NV / 8 v_add_f32 after each
 // Cycles per iteration (s_memtime, per wave) for 1 and 2 waves per SIMD.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -24,7 +26,7 @@ __global__ void k_coexec(int iters, float *out, long long *cyc) {
     const f2 pr = (f2){1e-7f * threadIdx.x, 2e-7f};
     const long long t0 = clock64();
     for (int it = 0; it < iters; ++it) {
-        if constexpr (MODE == 0 || MODE == 2) {
+        if constexpr (MODE == 0 || MODE == 2 || MODE == 4) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[c], 0, 0, 0);
@@ -32,8 +34,16 @@ __global__ void k_coexec(int iters, float *out, long long *cyc) {
 #pragma unroll
                     for (int j = 0; j < NV / 8; ++j)
                         asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(v[(c * (NV / 8) + j) & 15]) : "v"(pr));
+                } else if constexpr (MODE == 4) {
+#pragma unroll
+                    for (int j = 0; j < NV / 8; ++j)
+                        asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[(c * (NV / 8) + j) & 15][0]) : "v"(pr[0]));
                 }
             }
+        } else if constexpr (MODE == 3) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j)
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[j & 15][0]) : "v"(pr[0]));
         } else {
 #pragma unroll
             for (int j = 0; j < NV; ++j)
@@ -78,6 +88,10 @@ int main() {
                "mfma8+pk64 %.1f | pk_add x16 %.1f | mfma8+pk16 %.1f cycles/iteration/wave\n", w,
                run<0, 8>(w, iters), run<1, 32>(w, iters), run<2, 32>(w, iters), run<1, 64>(w, iters),
                run<2, 64>(w, iters), run<1, 16>(w, iters), run<2, 16>(w, iters));
+        printf("waves/SIMD %d: v_add x32 %.1f | mfma8+add32 %.1f | v_add x64 %.1f | mfma8+add64 %.1f | "
+               "v_add x16 %.1f | mfma8+add16 %.1f cycles/iteration/wave\n", w,
+               run<3, 32>(w, iters), run<4, 32>(w, iters), run<3, 64>(w, iters), run<4, 64>(w, iters),
+               run<3, 16>(w, iters), run<4, 16>(w, iters));
     }
     return 0;
 }
