@@ -9,13 +9,20 @@ streams get a per-class subclass (cached, same name) whose Module entry points t
 parameters first wait for that model's own block of rows:
 
     forward / __call__, parameters, named_parameters, state_dict, load_state_dict, _apply (.to,
-    .cuda, .float, ...)
+    .cuda, .float, ...), and pickling / deepcopy (__reduce_ex__)
 
 A wait is one event synchronize of the model's row block (a no-op once the block is back), and it
 is skipped entirely while no round is pending.  Reads through tensor references taken BEFORE the
 round (a cached `list(model.parameters())`) bypass any Module method and are not covered:
 call niidmix.d_sgd.synchronize() first.  NIIDMIX_READ_GUARD=0 disables the guard.
+
+Pickling.  A guarded model pickles (torch.save, pickle, a torch.multiprocessing queue, deepcopy)
+as an instance of its ORIGINAL class: __reduce_ex__ waits for the row, then names the base class,
+so the unpickled model is a plain model holding the mixed values.  The row / slab tags live in
+module-level weak dictionaries keyed by the model, never in the model's __dict__, so no weakref or
+engine reference travels with a pickled or copied model (a copy is never taken for the row).
 """
+import copyreg
 import os
 import weakref
 
@@ -23,16 +30,25 @@ import weakref
 stats = {"waits": 0}
 _classes = {}
 _suspend = [0]
+# model -> (weakref to the owning ResidentRound, row, first parameter's data_ptr)
+_row_tags = weakref.WeakKeyDictionary()
+# model -> (weakref to the owning NodeSlab, row, first parameter's data_ptr)
+_slab_tags = weakref.WeakKeyDictionary()
 
 
 def enabled():
     return os.environ.get("NIIDMIX_READ_GUARD", "1") != "0"
 
 
+def row_tag(model):
+    """The (engine ref, row, first parameter pointer) tag install() gave `model`, or None."""
+    return _row_tags.get(model)
+
+
 def _wait(model):
     if _suspend[0]:
         return
-    tag = model.__dict__.get("_niidmix_row")
+    tag = _row_tags.get(model)
     if tag is None:
         return
     ref, i = tag[0], tag[1]
@@ -43,10 +59,18 @@ def _wait(model):
 
 
 def _stale(model):
-    tag = model.__dict__.get("_niidmix_row")
+    tag = _row_tags.get(model)
     eng = tag[0]() if tag is not None else None
     if eng is not None:
         eng.fresh = False
+
+
+def _as_base(obj, g, cls):
+    if obj is g:
+        return cls
+    if isinstance(obj, tuple):
+        return tuple(_as_base(o, g, cls) for o in obj)
+    return obj
 
 
 def guarded_class(cls):
@@ -83,9 +107,23 @@ def guarded_class(cls):
         _stale(self)
         return cls._apply(self, *a, **k)
 
+    def __reduce_ex__(self, protocol):
+        # pickle / torch.save / deepcopy read the parameters: wait for the row, then reduce as
+        # the base class (the guarded class is not importable under its name)
+        _wait(self)
+        rv = super(g, self).__reduce_ex__(protocol)
+        if not isinstance(rv, tuple) or len(rv) < 2:
+            return rv
+        if rv[0] is copyreg.__newobj__ and rv[1] == (g,):
+            # the pickler insists that __newobj__'s class is the object's own: rebuild through
+            # the stdlib's object.__new__(cls) instead (no niidmix import needed to unpickle)
+            return (copyreg._reconstructor, (cls, object, None)) + rv[2:]
+        return (rv[0], _as_base(rv[1], g, cls)) + rv[2:]
+
     g = type(cls.__name__, (cls,), {
         "forward": forward, "parameters": parameters, "named_parameters": named_parameters,
         "state_dict": state_dict, "load_state_dict": load_state_dict, "_apply": _apply,
+        "__reduce_ex__": __reduce_ex__,
         "__module__": cls.__module__, "__qualname__": getattr(cls, "__qualname__", cls.__name__),
         "_niidmix_guarded": True})
     _classes[cls] = g
@@ -103,33 +141,33 @@ def install(models, engine):
     """Tag `models` as rows of `engine` (row i = models[i]; engine: an object with .pending,
     .wait_row(i) and .fresh -- niidmix.slab.ResidentRound -- held weakly) and, unless
     NIIDMIX_READ_GUARD=0, guard them.  The tag also records where the model's first parameter
-    lives (a slab view), so a deepcopy of the model -- which copies the tag -- is never taken for
-    the row itself (resident_rows)."""
+    lives (a slab view), so a model whose parameters were re-pointed elsewhere is no longer taken
+    for the row (resident_rows)."""
     ref = weakref.ref(engine)
     on = enabled()
     for i, m in enumerate(models):
         if on:
             m.__class__ = guarded_class(type(m))
-        m.__dict__["_niidmix_row"] = (ref, i, first_param_ptr(m))
+        _row_tags[m] = (ref, i, first_param_ptr(m))
 
 
 def resident_rows(models):
     """(engine, rows) when every model is a tagged, still slab-backed row of ONE engine, else
     None."""
-    return _rows_of(models, "_niidmix_row")
+    return _rows_of(models, _row_tags)
 
 
 def tag_slab(models, slab):
     """Record that models[i]'s parameters are row i of the pinned host slab `slab` (NodeSlab)."""
     ref = weakref.ref(slab)
     for i, m in enumerate(models):
-        m.__dict__["_niidmix_slab"] = (ref, i, first_param_ptr(m))
+        _slab_tags[m] = (ref, i, first_param_ptr(m))
 
 
-def _rows_of(models, key):
+def _rows_of(models, tags):
     owner, rows = None, []
     for m in models:
-        tag = m.__dict__.get(key)
+        tag = tags.get(m)
         if tag is None:
             return None
         e = tag[0]()
@@ -142,13 +180,14 @@ def _rows_of(models, key):
 
 def slab_rows(models):
     """(NodeSlab, rows) when every model is a still-backed row of ONE parameter slab, else None."""
-    return _rows_of(models, "_niidmix_slab")
+    return _rows_of(models, _slab_tags)
 
 
 def strip(model):
-    """Drop the row and slab tags of a copy (setup.model.average's deepcopy of models[0])."""
-    model.__dict__.pop("_niidmix_row", None)
-    model.__dict__.pop("_niidmix_slab", None)
+    """Drop any row / slab tag of `model` (setup.model.average's deepcopy of models[0]: tags are
+    never copied, so this only guards against a caller handing back a tagged model itself)."""
+    _row_tags.pop(model, None)
+    _slab_tags.pop(model, None)
     return model
 
 

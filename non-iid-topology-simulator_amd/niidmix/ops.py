@@ -778,8 +778,10 @@ class Mixer:
 
     def _build_dense(self):
         self.w_dense = torch.from_numpy(self.csr.dense()).to(self.device)
-        # W^T split into bf16 planes once per topology (the bf16x6 GEMM, kernel "dense")
-        self.w_split = dense_split_w(self.w_dense) if self.w_dense.is_cuda else None
+        # W^T split into bf16 planes once per topology (the bf16x6 GEMM, kernel "dense"), when
+        # the split fits the GEMM's 32-bit offsets (else the fp32 GEMM serves the graph)
+        self.w_split = dense_split_w(self.w_dense) \
+            if self.w_dense.is_cuda and b6_fits(self.n) else None
 
     def device_layout(self):
         """(perm, block_cols): the device-resident layout the factored kernels stream best, measured
@@ -877,7 +879,7 @@ class Mixer:
         if self.factored_safe and (x is None or _clique_ok(x)) and (out is None or _clique_ok(out)):
             return "clique"
         if self.dense:
-            return "dense"
+            return "dense" if b6_fits(self.n, x) else "dense-f32"
         if self.plan is not None and self.tlds is not None and (x is None or _lds_ok(x)) and \
                 (out is None or _lds_ok(out)):
             return "tile-lds-fast"               # clique graph with removed edges
@@ -944,12 +946,24 @@ class Mixer:
                        self.plan.max_clique_res)
         elif k == "dense":
             # bf16 matrix cores, fp32-accurate by three-term splits: 2.7x the fp32 MFMA's rate
+            _req(b6_fits(self.n, x), "kernel 'dense' (bf16x6): 16 rows of the slab or the "
+                 "split W exceed 2^31 B; use 'dense-f32'")
             mix_dense_b6(x, self.w_split, self.row_ptr, self.col, self.val, out)
         elif k == "dense-f32":
             mix_dense(x, self.w_dense, self.row_ptr, self.col, self.val, out)
         else:
             raise ValueError(f"unknown kernel {k!r}")
         return out
+
+
+def b6_fits(n, x=None):
+    """The bf16x6 GEMM's limits (niidmix_mix_dense_bf16x6_f32, niidmix.hip:4428): the split W
+    (2 B x niidmix_dense_split_elems(n)) and 16 rows of x's leading dimension below 2^31 B.  Host
+    arithmetic only (no GPU call)."""
+    lim = 0x7fffffff
+    if 2 * int(_lib.lib.niidmix_dense_split_elems(int(n))) >= lim:
+        return False
+    return x is None or 16 * _ld(x) * 4 < lim
 
 
 # member rows from which the launcher picks the multi-clique tile (niidmix.hip kQRowsMin)

@@ -55,21 +55,38 @@ class NodeSlab:
         self.p = sum(k for _, k in shapes)
         pin = pin and torch.cuda.is_available()
         self.host = torch.empty((self.n, self.p), dtype=torch.float32, pin_memory=pin)
+        # a parameter gets a tensor over its own stretch of the slab with a storage of its own
+        # size (torch.from_numpy over a slice): pickle.dumps(model.state_dict()) -- the reference
+        # logger, logger.py:139,254 -- and torch.save serialise a tensor's WHOLE storage, which for
+        # a plain view would be the whole [N, P] slab per node
+        arr = self.host.numpy()
         with torch.no_grad():
             for i, m in enumerate(models):
                 off = 0
                 for q, (shape, k) in zip(m.parameters(), shapes):
-                    view = self.host[i, off:off + k]
                     if grads:
+                        view = self.host[i, off:off + k]
                         if q.grad is None:
                             view.zero_()
                         else:
                             view.copy_(q.grad.detach().reshape(-1))
                         q.grad = view.view(shape)
                     else:
+                        view = torch.from_numpy(arr[i, off:off + k])
                         view.copy_(q.detach().reshape(-1))
                         q.data = view.view(shape)
                     off += k
+        # per model: (owning module, name, parameter) of every parameter in parameters() order
+        # (shared parameters once, at their first place), for owns()
+        self._slots = []
+        for m in models:
+            seen, slots = set(), []
+            for mod in m.modules():
+                for name, q in mod._parameters.items():
+                    if q is not None and id(q) not in seen:
+                        seen.add(id(q))
+                        slots.append((mod, name, q))
+            self._slots.append(slots)
         if not grads:
             from .guard import tag_slab
             tag_slab(models, self)
@@ -85,11 +102,16 @@ class NodeSlab:
             for i, m in enumerate(models):
                 if m is not self.models[i]:
                     return False
-                for q in m.parameters():
+                # every parameter, not just the first: one handed to a torch.multiprocessing queue
+                # is moved to shared memory on its own (storage per parameter), and one replaced
+                # by a new Parameter object is no longer a slab row (no module walk: ~0.5 us per
+                # parameter)
+                ptr = base + i * self.p * 4
+                for (mod, name, q), (_, k) in zip(self._slots[i], self.shapes):
                     t = q.grad if self.grads else q
-                    if t is None or t.data_ptr() != base + i * self.p * 4:
+                    if mod._parameters.get(name) is not q or t is None or t.data_ptr() != ptr:
                         return False
-                    break
+                    ptr += k * 4
         return True
 
 

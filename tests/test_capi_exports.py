@@ -84,6 +84,14 @@ def test_argument_errors_without_gpu():
     assert rc == _lib.EALIAS
     rc = L.niidmix_dense_split_w(4096, 4, 4096 + 16, None)
     assert rc == _lib.EALIAS         # w and its split overlap
+    # the bf16x6 GEMM's 32-bit offsets -- 16 rows of ld_x (ld_x >= 2^25) or a split
+    # W of 2^31 B (n = 19 000) -- are refused, never launched (niidmix.ops.b6_fits avoids them)
+    ld = 1 << 25
+    rc = L.niidmix_mix_dense_bf16x6_f32(base, ld, base + 4 * 4 * ld, ld, 4, 8, 1 << 24, 8, 8, 8, None)
+    assert rc == _lib.EUNSUPPORTED
+    rc = L.niidmix_mix_dense_bf16x6_f32(base, 8, base + 4 * 8 * 19000, 8, 19000, 8, 1 << 24, 8, 8, 8,
+                                        None)
+    assert rc == _lib.EUNSUPPORTED
     tp = _lib.TilePlanC(1, 12, 0, 8, 8, 8, 8, 8, 8)
     rc = L.niidmix_mix_tile_f32(16, 4, 1024, 4, 1, 4, ctypes.byref(tp), 0, None)
     assert rc == _lib.EUNSUPPORTED   # tile height 12
@@ -141,3 +149,25 @@ def test_argument_errors_without_gpu():
     assert S(18, 64, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 0, None) == _lib.EUNSUPPORTED     # x not 4-B aligned
     assert S(16, 64, 1 << 30, 64, 2, 64, 3, 8, 8, 8, 16, None) == _lib.EINVAL         # unknown mode
     assert S(16, 64, 1 << 30, 64, 0, 64, 3, 8, 8, 8, 0, None) == _lib.OK              # no rows
+
+
+def test_kernel_for_respects_bf16x6_limits():
+    """Mixer.kernel_for('fast') picks the bf16x6 GEMM ('dense') for a dense W only
+    within its limits (niidmix.ops.b6_fits: split W and 16 rows of the slab under 2^31 B), else the
+    fp32 MFMA GEMM ('dense-f32'), which has none.  Host arithmetic only."""
+    import numpy as np
+    import torch
+    from niidmix import ops
+    n = 64
+    w = np.random.default_rng(0).random((n, n)).astype(np.float32)
+    w /= w.sum(0, keepdims=True)
+    rp = np.arange(n + 1, dtype=np.int64) * n
+    col = np.concatenate([[i] + [j for j in range(n) if j != i] for i in range(n)]).astype(np.int32)
+    m = ops.Mixer(csr=ops.csr_from_numpy(rp, col, w[col, np.repeat(np.arange(n), n)]), device="cpu")
+    assert m.kernel_for("fast") == "dense"
+    ok = torch.empty_strided((2, 8), ((1 << 25) - 64, 1), device="meta")
+    wide = torch.empty_strided((2, 8), (1 << 25, 1), device="meta")
+    assert m.kernel_for("fast", ok) == "dense"
+    assert m.kernel_for("fast", wide) == "dense-f32"
+    assert m.kernel_for("fast", ok, wide) == "dense"        # y is addressed in 64 bits
+    assert ops.b6_fits(18000) and not ops.b6_fits(19000)

@@ -246,6 +246,24 @@ def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypat
         assert not any(pend)
 
 
+class RingNet(torch.nn.Module):
+    """The linear MNIST-shaped node model (module level: picklable by reference)."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc = torch.nn.Linear(784, 10)
+
+    def forward(self, x, params):
+        return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
+
+
+def _handoff_child(conn):
+    """torch.multiprocessing child: receive a model, send back its class name and weight."""
+    m = conn.recv()
+    conn.send((type(m).__name__, type(m).__module__, m.fc.weight.detach().numpy().copy()))
+    conn.close()
+
+
 def _ring_training_setup(n, seed=1337):
     from niidmix import d_sgd
     from niidmix.topology import mh_csr
@@ -258,20 +276,12 @@ def _ring_training_setup(n, seed=1337):
                             "initial-averaging": False, "clique-gradient": False,
                             "unbiased-gradient": False, "deferred-writeback": True}}
 
-    class Net(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.fc = torch.nn.Linear(784, 10)
-
-        def forward(self, x, params):
-            return torch.nn.functional.log_softmax(self.fc(x.view(-1, 784)), dim=1)
-
     g = torch.Generator().manual_seed(7)
     data = [(torch.rand(1, 28, 28, generator=g), int(torch.randint(0, 10, (1,), generator=g)))
             for _ in range(n * 200)]
     nodes = []
     for r in range(n):
-        mdl = Net()
+        mdl = RingNet()
         nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
                       "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
     edges = {r: [(r + 1) % n, (r - 1) % n] for r in range(n)}
@@ -282,12 +292,15 @@ def _ring_training_setup(n, seed=1337):
 def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
     """a driver that reads models on rounds _deferred_ok did NOT predict (no
     logging configured, so every round returns with the write-back in flight; the D2H is held back
-    ~50 ms by NIIDMIX_D2H_DELAY_CYCLES) gets the MIXED parameters through state_dict(), forward()
-    and parameters() -- niidmix.guard waits for the model's own rows -- bitwise the reference loop
-    doing the mixing.  With the guard off (NIIDMIX_READ_GUARD=0) the same reads see stale rows,
+    ~50 ms by NIIDMIX_D2H_DELAY_CYCLES) gets the MIXED parameters through state_dict(), forward(),
+    parameters(), pickle, torch.save / torch.load of the whole model and a torch.multiprocessing
+    hand-off (each returns the ORIGINAL class) -- niidmix.guard waits for the
+    model's own rows -- bitwise the reference loop doing the mixing.  With the guard off (NIIDMIX_READ_GUARD=0) the same reads see stale rows,
     which shows the test can tell the two apart."""
+    import io
+    import pickle
     from niidmix import d_sgd, guard
-    n, rounds = 16, 4
+    n, rounds = 16, 6
     monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")
     monkeypatch.setenv("NIIDMIX_D2H_DELAY_CYCLES", str(100_000_000))
 
@@ -309,13 +322,34 @@ def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
                 # the unpredicted reader, right after next_step: one entry point per round
                 r = (5 * k + 3) % n
                 mdl = nodes[r]["model"]
-                if k % 3 == 0:
+                if k == 0:
                     w = mdl.state_dict()["fc.weight"].clone()
-                elif k % 3 == 1:
+                elif k == 1:
                     w = next(mdl.parameters()).detach().clone()
-                else:
+                elif k == 2:
                     mdl.forward(torch.zeros(1, 784), params)
                     w = mdl.fc.weight.detach().clone()
+                elif k == 3:                          # pickle
+                    c = pickle.loads(pickle.dumps(mdl))
+                    assert type(c) is RingNet
+                    w = c.fc.weight.detach().clone()
+                elif k == 4:                          # a whole-model checkpoint
+                    buf = io.BytesIO()
+                    torch.save(mdl, buf)
+                    buf.seek(0)
+                    c = torch.load(buf, weights_only=False)   # our own file
+                    assert type(c) is RingNet and buf.getbuffer().nbytes < 64 << 10
+                    w = c.fc.weight.detach().clone()
+                else:                                 # a torch.multiprocessing hand-off
+                    ctx = torch.multiprocessing.get_context("spawn")
+                    a, b = ctx.Pipe()
+                    pr = ctx.Process(target=_handoff_child, args=(b,))
+                    pr.start()
+                    a.send(mdl)
+                    name, mod, w = a.recv()
+                    w = torch.from_numpy(w)
+                    pr.join(60)
+                    assert pr.exitcode == 0 and (name, mod) == ("RingNet", RingNet.__module__)
                 seen.append(w)
                 d_sgd.synchronize()
         finally:
@@ -723,7 +757,7 @@ def test_logger_hooks_read_resident_slab(gpu, monkeypatch, tmp_path):
     by the reference itself (make_golden.py --logger): the round bitwise, the consensus event's
     avg/max/min/norm within 1e-5 and std within 1e-4 relative, the global models (all nodes, a
     nodes_to_log subset, node 0 alone) bitwise."""
-    from niidmix import d_sgd
+    from niidmix import d_sgd, guard
     from niidmix import logger as nl
     g = load_golden("logger_round_dcliques300_p520")
     lg, sm = _fake_reference_modules(monkeypatch, tmp_path)
@@ -758,7 +792,7 @@ def test_logger_hooks_read_resident_slab(gpu, monkeypatch, tmp_path):
         assert nl.last_source["average"] == "resident"
         flat = torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy()
         assert oracle_bitwise(flat, g[key]), key
-        assert "_niidmix_row" not in c.__dict__
+        assert guard.row_tag(c) is None and type(c) is FlatModel     # a plain copy
     # a guarded write (load_state_dict) makes the device copy stale: the next read stacks
     models[5].load_state_dict(models[5].state_dict())
     assert not eng.resident.fresh

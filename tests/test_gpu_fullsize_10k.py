@@ -3,14 +3,16 @@ layouts and launch paths as bench.py --config dcliques10000 and the multi-GPU st
 
   * the single-GPU fast round exactly as benched: relabeled (clique-contiguous) rows, column-blocked
     VMM slabs [16384, 10000, 64] (the multi-clique tile's layout: a 64-column chunk of every row is
-    one contiguous stretch), the clique kernel (k_mix_clique_q); the first, middle and last blocks
-    against the oracle (the last starts 1.05e10 elements into the slab: past 2^31, 2^32 and 2^33),
-    plus column-sum preservation over every block; and the same on the round-2 layout
-    [4096, 10000, 256] (NIIDMIX_Q_BLOCK_COLS=256);
+    one contiguous stretch), the clique kernel (k_mix_clique_q); EVERY element against the exact
+    kernel's round of the same input (1e-5 condition-aware, tests/fullcheck.py), 32 random blocks
+    plus the first and last against the oracle (the last starts 1.05e10 elements into the slab:
+    past 2^31, 2^32 and 2^33), plus column-sum preservation over every block; and the same on the
+    round-2 layout [4096, 10000, 256] (NIIDMIX_Q_BLOCK_COLS=256);
   * the exact default (tile-lds-exact: since round 4 each clique's 99 inter-clique sources are
     register rows, 100 staged rows -> 128-column items; NIIDMIX_TLDS_REMOTE=0 stages all 199 rows ->
     96-column items) on row-major [10000, 2^20] slabs, bitwise on windows that straddle item
-    boundaries, the ragged last item and rows whose offsets exceed 2^33 elements;
+    boundaries, the ragged last item, rows whose offsets exceed 2^33 elements and 16 random
+    windows;
   * one rank of the 8000-node weak N=8 column-stripe shape (StripedMixer: 79 gateway terms per
     clique, B = 64), windows against the oracle and column sums over the whole stripe.
 
@@ -21,6 +23,8 @@ random_cliques.py:43-44 (fully-connected interclique by default), interclique.py
 import numpy as np
 import pytest
 import torch
+
+from fullcheck import check_blocked_every_element
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-5
@@ -75,9 +79,9 @@ def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod, monkeypatch
     m.mix_blocked(xb, yb, P_FULL)
     torch.cuda.synchronize()
     assert (kb - 1) * xb.stride(0) > (1 << 33)
-    for k in (0, kb // 2 - 1, kb - 1):
-        _check_fast(oracle_mod, m.csr, xb[k].cpu().numpy(), yb[k].cpu().numpy(), k)
     assert not torch.isnan(yb).any().item()
+    # every element against the exact kernel; 32 random blocks + first / last vs the oracle
+    check_blocked_every_element(m, xb, yb, P_FULL, oracle_mod, seed=22 + len(bc_env))
     assert _blocked_colsum_gap(xb, yb) < 2e-3
     del xb, yb
     _free()
@@ -104,7 +108,9 @@ def test_dcliques10000_tile_lds_exact_rowmajor(remote, dc10k, gpu, oracle_mod, m
     m(x, out=y, mode="exact")
     torch.cuda.synchronize()
     w = cw * 3
-    for c0 in (0, cw * 5461 - 40, P_FULL - w):
+    rng = np.random.default_rng(23)
+    picks = [int(c) for c in rng.integers(0, P_FULL - w, size=16)]
+    for c0 in [0, cw * 5461 - 40, P_FULL - w] + picks:
         xw = x[:, c0:c0 + w].cpu().numpy()
         ref = oracle_mod.mix_exact_c(xw, csr.row_ptr, csr.col, csr.val)
         assert oracle_mod.bitwise_equal(y[:, c0:c0 + w].cpu().numpy(), ref), c0

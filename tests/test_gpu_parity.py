@@ -353,17 +353,15 @@ def test_full_size_exact_windows(kernel, gpu, oracle_mod):
 
 
 def test_full_size_clique_windows_and_checksum(gpu, oracle_mod):
-    """Headline kernel at full size: windows vs oracle within tolerance, plus a size-independent
-    property over ALL columns: W is doubly stochastic, so column sums are preserved."""
+    """Headline kernel at full size on row-major slabs: EVERY element against the exact kernel's
+    round of the same input (1e-5 condition-aware, tests/fullcheck.py), 32 random 1024-column
+    windows plus the first and last against the oracle, and column sums over ALL columns (W is
+    doubly stochastic) as an extra check."""
+    from fullcheck import check_rowmajor_every_element
     p = 1 << 20
     g, m, x = _dcliques_full(gpu, p, seed=1)
     y = m(x, kernel="clique")
-    for c0, c1 in _windows(p):
-        xw = x[:, c0:c1].cpu().numpy()
-        ref = oracle_mod.mix_exact_c(xw, g["row_ptr"], g["col"], g["val"])
-        bound = oracle_mod.condition_bound(xw, g["row_ptr"], g["col"], g["val"])
-        ok, worst = oracle_mod.check_tolerance(y[:, c0:c1].cpu().numpy(), ref, bound, rtol=RTOL)
-        assert ok, worst
+    check_rowmajor_every_element(m, x, y, oracle_mod, seed=21)
     cs_x = x.double().sum(0)
     cs_y = y.double().sum(0)
     # column sums agree to fp32 accumulation accuracy of ~1000 terms of O(1)
@@ -756,6 +754,86 @@ def test_dense_b6_split_gemm(n, p, gpu, oracle_mod):
         ok, worst[k] = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
         assert ok, (k, worst[k])
     assert worst["dense"] <= 4 * max(worst["dense-f32"], 1e-7), worst
+
+
+FLT_MAX = float(np.finfo(np.float32).max)
+
+
+def _extreme_case(case, n, p, rng):
+    """(W, X) of one extreme-magnitude case for the bf16x6 GEMM (VERDICT r05 #1b)."""
+    w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)
+    x = rng.standard_normal((n, p))
+    if case == "column-scales":
+        # columns at 2^k, k in {-126, -120, -100, -60, 60, 100, 120} (2^-126 x N(0,1): subnormals)
+        ks = np.array([-126, -120, -100, -60, 60, 100, 120])
+        x = x * np.exp2(ks[np.arange(p) % len(ks)])[None, :]
+    elif case == "mixed-rows":
+        # every column mixes rows at 2^-100 and 2^100
+        x = x * np.where(np.arange(n) % 2 == 0, 2.0 ** -100, 2.0 ** 100)[:, None]
+    elif case == "near-flt-max":
+        # every other row within 2^-8 of FLT_MAX (random sign): its bf16 head may round to inf
+        big = FLT_MAX * (1.0 - rng.random((n, p)) * 2.0 ** -8) * np.sign(x)
+        x = np.where((np.arange(n) % 2 == 0)[:, None], big, x)
+    elif case == "tiny-w":
+        # W entries spread over 1e-30 .. 1
+        w = w * np.power(10.0, -30.0 * rng.random((n, n))).astype(np.float32)
+    elif case == "tiny-w-tiny-x":
+        w = w * np.power(10.0, -30.0 * rng.random((n, n))).astype(np.float32)
+        x = x * 2.0 ** -60
+    w = w / w.sum(0, keepdims=True)
+    return w.astype(np.float32), x.astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["column-scales", "mixed-rows", "near-flt-max", "tiny-w",
+                                  "tiny-w-tiny-x"])
+@pytest.mark.parametrize("n,p", [(257, 300), (1000, 1030)])
+def test_dense_b6_extreme_inputs(case, n, p, gpu, oracle_mod):
+    """The auto-selected bf16x6 GEMM (Mixer.kernel_for('fast') == 'dense' for a dense W with no
+    clique structure) on inputs whose split residues are not representable as assumed by the
+    well-scaled argument (niidmix.hip, k_mix_dense_b6 header): columns from 2^-126 (subnormal) to
+    2^120, columns mixing 2^+-100 rows, values within 2^-8 of FLT_MAX (bf16 head -> inf: the
+    non-finite guard carries the element), W entries down to 1e-30 (with and without tiny X);
+    ragged M, K (n % 16 != 0) and P tiles.  Within the 1e-5 condition-aware tolerance of the
+    oracle (the reference's fp32 loop, d_sgd.py:96-116 / model/__init__.py:19-24), like the fp32
+    MFMA kernel on the same inputs."""
+    ops = _ops()
+    rng = np.random.default_rng(sum(map(ord, case)) + n)
+    w, xn = _extreme_case(case, n, p, rng)
+    csr = ops.csr_from_numpy(*_dense_csr(w))
+    m = ops.Mixer(csr=csr, device=gpu)
+    assert m.kernel_for("fast") == "dense"
+    x = torch.from_numpy(xn).to(gpu)
+    with np.errstate(over="ignore", invalid="ignore"):
+        ref = oracle_mod.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
+        bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
+    worst = {}
+    for k in ("dense", "dense-f32"):
+        y = m(x, kernel=k).cpu().numpy()
+        ok, worst[k] = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+        assert ok, (case, k, worst[k])
+
+
+def test_dense_b6_tail_rows_not_read(gpu):
+    """on the last K-step the bf16x6 GEMM loads 16 rows from k0; rows past n must read
+    as zeros (buffer range check), never the memory after x.  x is the first n rows (n % 16 != 0)
+    of a buffer whose tail rows are NaN: the output must be bitwise that of the same x followed by
+    zero rows (a NaN read would send elements through the CSR recompute, whose bits differ)."""
+    ops = _ops()
+    rng = np.random.default_rng(5)
+    for n, p in ((257, 300), (1000, 1030)):
+        w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)
+        w /= w.sum(0, keepdims=True)
+        m = ops.Mixer(csr=ops.csr_from_numpy(*_dense_csr(w)), device=gpu)
+        kpad = -(-n // 16) * 16 + 16
+        xv = torch.from_numpy(rng.standard_normal((n, p)).astype(np.float32)).to(gpu)
+        bufs = {}
+        for tail in (0.0, float("nan")):
+            buf = torch.full((kpad, p), tail, device=gpu)
+            buf[:n] = xv
+            bufs[tail] = m(buf[:n], kernel="dense").cpu().numpy()
+        a, b = bufs[0.0], bufs[float("nan")]
+        assert not np.isnan(b).any()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), n
 
 
 @pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (257, 1030), (300, 70000)])

@@ -188,6 +188,107 @@ def test_read_guard_waits_for_own_row(monkeypatch):
     assert type(plain[0]) is Net
 
 
+def _handoff_child(conn):
+    """torch.multiprocessing child: receive a model, send back its class and flat parameters."""
+    m = conn.recv()
+    # numpy, not a tensor: a tensor would go back through a shared-memory fd that this process,
+    # about to exit, could no longer serve
+    conn.send((type(m), torch.cat([q.detach().reshape(-1) for q in m.parameters()]).numpy()))
+    conn.close()
+
+
+class _Round:
+    pending = True
+
+    def __init__(self):
+        self.waited = []
+
+    def wait_row(self, i):
+        self.waited.append(i)
+
+
+def test_slab_models_pickle_compact():
+    """A NodeSlab-backed model's parameters each have a storage of their own size: the reference
+    logger's pickle.dumps(model.state_dict()) (logger.py:139,254) and torch.save(model) write that
+    model only, not the whole [N, P] slab (a plain view would serialise its whole storage); the
+    tensors still alias the slab (an in-place update lands in it)."""
+    import io
+    import pickle
+    torch.manual_seed(3)
+    models = [torch.nn.Linear(100, 10) for _ in range(64)]
+    slab = NodeSlab(models, pin=False)
+    one = 1010 * 4
+    assert slab.host.numel() * 4 > 60 * one
+    m = models[17]
+    blob = pickle.dumps(m.state_dict())
+    assert len(blob) < 2 * one + 2048
+    sd = pickle.loads(blob)
+    assert torch.equal(sd["weight"], m.weight.detach()) and torch.equal(sd["bias"], m.bias.detach())
+    buf = io.BytesIO()
+    torch.save(m, buf)
+    assert buf.tell() < 2 * one + 4096
+    with torch.no_grad():
+        m.bias.add_(1.0)
+    assert torch.equal(slab.host[17, 1000:], m.bias.detach())
+    assert slab.owns(models)
+
+
+def test_guarded_model_pickles_as_base_class(monkeypatch):
+    """VERDICT r05 #5 / ADVICE r05: a guarded, slab-tagged model pickles -- pickle, torch.save /
+    torch.load, deepcopy, a torch.multiprocessing hand-off -- as its ORIGINAL class holding its
+    current values, after waiting for its own row while a round is pending; no tag travels with
+    the copy.  A hand-off moves the sent parameters to shared memory (torch.multiprocessing's own
+    semantics): the slab no longer owns the model, so the drop-in rebuilds its engine."""
+    import copy
+    import io
+    import pickle
+    from niidmix import guard
+    monkeypatch.delenv("NIIDMIX_READ_GUARD", raising=False)
+    torch.manual_seed(4)
+    models = [torch.nn.Linear(6, 4) for _ in range(5)]
+    slab = NodeSlab(models, pin=False)
+    eng = _Round()
+    guard.install(models, eng)
+    m = models[3]
+    assert type(m) is not torch.nn.Linear and isinstance(m, torch.nn.Linear)
+    assert guard.row_tag(m)[1] == 3 and guard.slab_rows(models)[1] == [0, 1, 2, 3, 4]
+    flat = slab.host[3].clone()
+
+    def check(c):
+        assert type(c) is torch.nn.Linear
+        assert torch.equal(torch.cat([c.weight.detach().reshape(-1), c.bias.detach()]), flat)
+        assert guard.row_tag(c) is None and guard.slab_rows([c]) is None
+
+    for rt in (lambda: pickle.loads(pickle.dumps(m)),
+               lambda: pickle.loads(pickle.dumps(m, protocol=1)),
+               lambda: copy.deepcopy(m), lambda: copy.copy(m)):
+        eng.waited.clear()
+        check(rt())
+        assert eng.waited == [3]
+    buf = io.BytesIO()
+    eng.waited.clear()
+    torch.save(m, buf)
+    assert eng.waited == [3]
+    buf.seek(0)
+    check(torch.load(buf, weights_only=False))     # a file this test wrote
+    eng.pending = False
+    eng.waited.clear()
+    check(pickle.loads(pickle.dumps(m)))
+    assert eng.waited == []
+    eng.pending = True
+    ctx = torch.multiprocessing.get_context("spawn")
+    a, b = ctx.Pipe()
+    pr = ctx.Process(target=_handoff_child, args=(b,))
+    pr.start()
+    eng.waited.clear()
+    a.send(m)
+    cls, got = a.recv()
+    pr.join(60)
+    assert pr.exitcode == 0 and cls is torch.nn.Linear and torch.equal(torch.from_numpy(got), flat)
+    assert eng.waited == [3]
+    assert not slab.owns(models) and guard.resident_rows(models) is None
+
+
 def test_logger_install_hooks_cpu(monkeypatch, tmp_path):
     """niidmix.logger.install_hooks (called by niidmix.d_sgd.init) routes the reference driver's
     Logger.log_consensus_distance always, and setup.model.average only with
