@@ -827,11 +827,11 @@ def test_dense_b6_tail_rows_not_read(gpu):
         kpad = -(-n // 16) * 16 + 16
         xv = torch.from_numpy(rng.standard_normal((n, p)).astype(np.float32)).to(gpu)
         bufs = {}
-        for tail in (0.0, float("nan")):
-            buf = torch.full((kpad, p), tail, device=gpu)
+        for tail in ("zero", "nan"):
+            buf = torch.full((kpad, p), 0.0 if tail == "zero" else float("nan"), device=gpu)
             buf[:n] = xv
             bufs[tail] = m(buf[:n], kernel="dense").cpu().numpy()
-        a, b = bufs[0.0], bufs[float("nan")]
+        a, b = bufs["zero"], bufs["nan"]
         assert not np.isnan(b).any()
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), n
 
