@@ -9,13 +9,14 @@ typedef float f32v __attribute__((ext_vector_type(32)));
 constexpr int ITERS = 4096;
 
 template <int KIND>
-__global__ __launch_bounds__(256) void k(float *out, float w, int sel) {
+__global__ __launch_bounds__(256) void k(float *out, float w, int sel, long long *tick) {
     f32v acc;
 #pragma unroll
     for (int i = 0; i < 32; ++i) acc[i] = (float)(threadIdx.x + i);
     f2 tp = {w, w * 2.f};
     float nz = -0.0f * w;
     const int idxv = (int)(threadIdx.x * 7 + sel) & 1023;
+    const long long c0 = clock64(), r0w = wall_clock64();
     for (int it = 0; it < ITERS; ++it) {
         asm volatile("" : "+v"(tp));
         if (KIND == 0) {            // 16 v_pk_add_f32
@@ -98,10 +99,17 @@ __global__ __launch_bounds__(256) void k(float *out, float w, int sel) {
             }
         }
     }
+    asm volatile("" :: "v"(acc));
+    const long long c1 = clock64(), r1w = wall_clock64();
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 32; ++i) s += acc[i];
     out[blockIdx.x * 256 + threadIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) {
+        const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+        tick[2 * wv] = c1 - c0;
+        tick[2 * wv + 1] = r1w - r0w;
+    }
 }
 
 static const char *names[] = {"16 pk_add (compiler)", "32 v_add_f32", "16 pk_add (asm)", "select path: 32 cndmask + 16 pk_add",
@@ -112,32 +120,46 @@ static const char *names[] = {"16 pk_add (compiler)", "32 v_add_f32", "16 pk_add
 static const int instrs[] = {16, 32, 16, 48, 16, 32, 16, 16, 48, 64, 16, 16, 16, 16};
 
 template <int KIND>
-void run(float *out, int blocks_per_cu) {
+void run(float *out, long long *tick, int blocks_per_cu) {
     int cus = 256;
     int blocks = cus * blocks_per_cu;                 // 4 waves per block -> blocks_per_cu waves/SIMD
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
-    k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a);
+    k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a, tick);
     hipEventRecord(a);
-    for (int r = 0; r < 5; ++r) k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a);
+    for (int r = 0; r < 5; ++r) k<KIND><<<blocks, 256>>>(out, 1.0001f, 0x5a5a, tick);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
     ms /= 5;
-    // wave-instructions per SIMD = waves/SIMD * ITERS * instrs
-    double per_simd = (double)blocks_per_cu * ITERS * instrs[KIND];
-    double cyc = ms * 1e-3 * 2.4e9;
-    printf("%-40s waves/SIMD %2d: %.3f ms, %.2f cyc/instr @2.4GHz (%.1f cyc per loop iteration per wave)\n",
-           names[KIND], blocks_per_cu, ms, cyc / per_simd, cyc / (blocks_per_cu * (double)ITERS));
+    // in-kernel: shader-clock cycles (clock64) and 100 MHz wall ticks (wall_clock64) per wave over
+    // the loop; with W waves sharing a SIMD, cycles per wave-instruction of SIMD issue =
+    // loop cycles / (W * ITERS * instrs)
+    const int waves = blocks * 4;
+    static long long h[2 * 256 * 16 * 4];
+    hipMemcpy(h, tick, sizeof(long long) * 2 * waves, hipMemcpyDeviceToHost);
+    double cyc = 0, wall = 0;
+    for (int i = 0; i < waves; ++i) { cyc += h[2 * i]; wall += h[2 * i + 1]; }
+    cyc /= waves; wall /= waves;
+    const double ghz = cyc / (wall * 10.0);           // wall ticks are 10 ns
+    const double per_instr = cyc / ((double)blocks_per_cu * ITERS * instrs[KIND]);
+    printf("%-44s waves/SIMD %2d: %.3f ms/launch, loop %.0f cyc @ %.2f GHz -> %.2f cyc per wave-instr"
+           " (%.2f by wall time @2.4GHz)\n", names[KIND], blocks_per_cu, ms, cyc, ghz, per_instr,
+           ms * 1e-3 * 2.4e9 / ((double)blocks_per_cu * ITERS * instrs[KIND]));
 }
 
 int main() {
     float *out;
+    long long *tick;
     hipMalloc(&out, 256 * 16 * 256 * sizeof(float));
-    for (int occ : {2, 4, 8}) {
-        run<0>(out, occ); run<4>(out, occ); run<12>(out, occ); run<13>(out, occ);
+    hipMalloc(&tick, 2 * 256 * 16 * 4 * sizeof(long long));
+    // back-to-back packed and scalar fp32 adds at one and two waves per SIMD
+    for (int occ : {1, 2, 4}) {
+        run<2>(out, tick, occ); run<1>(out, tick, occ); run<0>(out, tick, occ); run<7>(out, tick, occ);
     }
+    for (int occ : {2, 4}) { run<4>(out, tick, occ); run<3>(out, tick, occ); }
     hipFree(out);
+    hipFree(tick);
     return 0;
 }
