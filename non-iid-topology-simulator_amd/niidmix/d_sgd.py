@@ -180,6 +180,38 @@ def gradient(nodes, topology, params):
         nodes[r]["optimizer"].step()
 
 
+_sgd_checked = {}
+# node lists whose device-step buffers did not fit in HBM (the CPU steps them)
+_no_device_step = set()
+
+
+def _device_step_ok(params, nodes):
+    """The plain round's optimizer step may run on the device (_FusedEngine(plain=True)): every
+    node's optimizer is the plugin's plain SGD (optimizer() above, momentum 0: no state, p += -lr g)
+    over exactly its model's parameters, at params' learning rate; NIIDMIX_DEVICE_STEP=0 disables
+    it (the CPU steps, as rounds 1-5 did)."""
+    if os.environ.get("NIIDMIX_DEVICE_STEP", "1") == "0" or not _resident_ok() or \
+            id(nodes) in _no_device_step:
+        return False
+    lr = float(params["algorithm"]["learning-rate"])
+    for nd in nodes:
+        opt = nd.get("optimizer")
+        if type(opt) is not torch.optim.SGD or len(opt.param_groups) != 1:
+            return False
+        g = opt.param_groups[0]
+        if (float(g["lr"]) != lr or g["momentum"] != 0 or g["dampening"] != 0 or
+                g["weight_decay"] != 0 or g["nesterov"] or g.get("maximize", False)):
+            return False
+        hit = _sgd_checked.get(id(opt))
+        if hit is None or hit[0] is not opt or hit[1] is not nd["model"]:
+            with guard.suspended():
+                mine = list(nd["model"].parameters())
+            if len(g["params"]) != len(mine) or any(a is not b for a, b in zip(g["params"], mine)):
+                return False
+            _sgd_checked[id(opt)] = (opt, nd["model"])
+    return True
+
+
 def _fused_ok(params):
     """The fused device round applies when gradients are averaged and the optimizer step is plain
     SGD (momentum 0: the reference's default, d_sgd.py:262-263); NIIDMIX_FUSED=0 disables it."""
@@ -193,19 +225,30 @@ class _FusedEngine:
     (niidmix.slab.ResidentRound with fused_op: each node's parameter and gradient rows go to the
     GPU right after its backward(), the mixed parameters and averaged gradients come back while
     the next round trains) or windowed (FusedRoundRunner); one column stripe per GPU when several
-    are visible (niidmix.slab.MultiDeviceRound)."""
+    are visible (niidmix.slab.MultiDeviceRound).
 
-    def __init__(self, nodes, topology, params, devices):
+    plain=True: the plain D-SGD round with its optimizer step on the device (no gradient
+    averaging; resident engine only): each node's gradient row goes up right after its backward(),
+    the SGD step p += (-lr) g (d_sgd.py:51-52, bitwise torch's CPU SGD) runs on the device-resident
+    parameters, then the mixing.  The gradients are views of a pinned slab filled with -0.0 before
+    each backward (accumulate_grad adds in place: -0 + g = g bit for bit, every g, where a +0 fill
+    would turn a -0 gradient into +0).  While the models were not written between rounds (the
+    resident round's `fresh` flag, guarded writes, and the parameters' version counters) the
+    parameters stay on the device: only gradients go H2D; otherwise they go up with them."""
+
+    def __init__(self, nodes, topology, params, devices, plain=False):
         from .gradient import GradMean, build_grad_plan
         from .ops import Mixer
         from .slab import FusedRoundRunner, MultiDeviceRound, NodeSlab, ResidentRound, fused_op
         self.topology = topology
         self.weights_id = id(topology.get("weights"))
-        self.key = _grad_key(params) + (float(params["algorithm"]["learning-rate"]),)
+        self.plain = plain
+        self.key = _grad_key(params) + (float(params["algorithm"]["learning-rate"]), plain)
         models = [n["model"] for n in nodes]
         self.slab = NodeSlab(models)
         self.gslab = NodeSlab(models, grads=True)
-        self.plan = build_grad_plan(len(nodes), topology, params)
+        self.plan = None if plain else build_grad_plan(len(nodes), topology, params)
+        stepped = list(range(len(nodes))) if plain else self.plan.stepped
         csr = to_csr(topology)
         if csr.n != self.slab.n:
             raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
@@ -213,27 +256,51 @@ class _FusedEngine:
         lr = params["algorithm"]["learning-rate"]
 
         n, p = self.slab.n, self.slab.p
-        wb = os.environ.get("NIIDMIX_GRAD_WRITEBACK", "1") != "0"
+        # the plain round's gradients are the nodes' own: nothing to write back
+        wb = not plain and os.environ.get("NIIDMIX_GRAD_WRITEBACK", "1") != "0"
         self.resident = None
         self.runner = None
+        self._ver = None
+        self.param_uploads = 0          # rounds whose parameters went H2D (tests)
         if _resident_ok() and ResidentRound.fits(n, p, devices, buffers=4 if wb else 3):
             self.resident = ResidentRound(
-                lambda dev, part: fused_op(dev, part, GradMean(self.plan, dev), self.plan.stepped,
-                                           lr, self.mixer if dev == devices[0] else self.mixer.to(dev)),
+                lambda dev, part: fused_op(dev, part, None if plain else GradMean(self.plan, dev),
+                                           stepped, lr,
+                                           self.mixer if dev == devices[0] else self.mixer.to(dev)),
                 n, p, devices, block=_row_block(), n_in=2, n_out=2 if wb else 1)
             self.outs = (self.slab.host, self.gslab.host) if wb else (self.slab.host,)
             guard.install(models, self.resident)
-        else:
+        elif not plain:
             def make(dev, n, cols):
                 mixer = self.mixer if dev == devices[0] else self.mixer.to(dev)
                 return FusedRoundRunner(GradMean(self.plan, dev), self.plan.stepped, lr, mixer, n,
                                         cols, dev, window=_window())
             self.runner = MultiDeviceRound(make, n, p, devices)
 
+    @property
+    def kind(self):
+        return "own gradient" if self.plain else self.plan.kind
+
+    def params_resident(self):
+        """The device holds the models' current parameters: the last round's mixed output, with no
+        write to the models since (guarded writes clear `fresh`; the version counters catch writes
+        through the parameters, e.g. an optimizer step or p.add_ under no_grad)."""
+        rr = self.resident
+        return (rr is not None and rr.fresh and self._ver is not None
+                and self.slab.version() == self._ver)
+
+    def clear_grad_row(self, i):
+        """Before node i's backward: its gradient views to -0.0 (see the class docstring)."""
+        self.gslab.host[i].fill_(-0.0)
+
     # the row-streamed round (resident engine only)
     def begin_round(self):
         if self.resident is not None:
-            self.resident.begin(self.slab.host, self.gslab.host, outs=self.outs)
+            if self.params_resident():
+                self.resident.begin(None, self.gslab.host, outs=self.outs, resident_in0=True)
+            else:
+                self.param_uploads += 1
+                self.resident.begin(self.slab.host, self.gslab.host, outs=self.outs)
 
     def row_ready(self, i):
         if self.resident is not None:
@@ -252,6 +319,7 @@ class _FusedEngine:
             if self.resident.hosts is None:
                 self.begin_round()                    # nothing streamed: every row goes up now
             self.resident.mix(mode, timing=timing)
+            self._ver = self.slab.version()
             if not defer:
                 self.resident.wait_all()
                 return self.resident.last_timing
@@ -259,11 +327,29 @@ class _FusedEngine:
         self.runner.run(self.slab.host, self.gslab.host, mode=mode, timing=timing)
         return self.runner.last_timing
 
-    def valid_for(self, nodes, topology, params):
+    def same_models(self, nodes, params):
         models = [n["model"] for n in nodes]
+        return (_grad_key(params) + (float(params["algorithm"]["learning-rate"]), self.plain)
+                == self.key and self.slab.owns(models) and self.gslab.owns(models))
+
+    def valid_for(self, nodes, topology, params):
         return (topology is self.topology and id(topology.get("weights")) == self.weights_id
-                and _grad_key(params) + (float(params["algorithm"]["learning-rate"]),) == self.key
-                and self.slab.owns(models) and self.gslab.owns(models))
+                and self.same_models(nodes, params))
+
+    def set_topology(self, topology):
+        """A new graph for the same nodes (plain rounds, random-graph --randomize): only the
+        mixing operator changes; the slabs and the resident device buffers are kept."""
+        from .ops import Mixer
+        csr = to_csr(topology)
+        if csr.n != self.slab.n:
+            raise ValueError(f"topology has {csr.n} nodes, {self.slab.n} models given")
+        self.wait_all()                  # the last round's kernel may still read the old Mixer
+        dev0 = self.resident.parts[0]["dev"]
+        self.mixer = Mixer(csr=csr, cliques=topology.get("cliques"), device=dev0)
+        for pt in self.resident.parts:
+            pt["mixer"] = self.mixer if pt["dev"] == dev0 else self.mixer.to(pt["dev"])
+        self.topology = topology
+        self.weights_id = id(topology.get("weights"))
 
 
 _fused_engines = {}
@@ -281,12 +367,15 @@ def fused_round(nodes, topology, params):
         logging.info("  fused round: %s", t)
 
 
-def _fused_engine(nodes, topology, params):
-    key = id(nodes)
+def _fused_engine(nodes, topology, params, plain=False):
+    key = (id(nodes), plain)
     eng = _fused_engines.get(key)
+    if plain and eng is not None and not eng.valid_for(nodes, topology, params) and \
+            eng.same_models(nodes, params):
+        eng.set_topology(topology)                   # same nodes, new graph (--randomize)
     if eng is None or not eng.valid_for(nodes, topology, params):
         synchronize()
-        eng = _FusedEngine(nodes, topology, params, _devices(nodes))
+        eng = _FusedEngine(nodes, topology, params, _devices(nodes), plain=plain)
         _fused_engines.pop(key, None)
         _fused_engines[key] = eng
         while len(_fused_engines) > MAX_ENGINES:
@@ -411,6 +500,8 @@ class _Engine:
 
 
 _engines = {}
+# the engine that ran the last row-streamed next_step round of a node list (round_engine)
+_last_round = {}
 # engines (pinned slab + device buffers) kept per node list, the most recent ones
 MAX_ENGINES = int(os.environ.get("NIIDMIX_MAX_ENGINES", 4))
 
@@ -420,6 +511,12 @@ def _mode(params):
     if mode not in ("exact", "fast"):
         raise ValueError(f"unknown mixing mode {mode!r}")
     return mode
+
+
+def round_engine(nodes):
+    """The engine (_Engine or _FusedEngine, with .resident) whose row-streamed round last ran for
+    this node list in next_step, or None."""
+    return _last_round.get(id(nodes))
 
 
 def synchronize():
@@ -619,11 +716,20 @@ def next_step(state, params, rundir):
     # plain D-SGD (own gradient, then mixing): the row-streamed round — each node's rows go to the
     # GPU right after its optimizer.step() and come back while the next round trains
     streamed = not sample and not _averages_gradients(params) and _row_streamed(params)
-    eng = _engine(active, topology) if streamed else None
+    feng = None
+    if streamed and _device_step_ok(params, active):
+        # ... with the optimizer step on the device: each node's gradient row goes up right after
+        # its backward(), the parameters stay resident (_FusedEngine(plain=True))
+        feng = _fused_engine(active, topology, params, plain=True)
+        if feng.resident is None:                 # the buffers do not fit: CPU step, windowed
+            _fused_engines.pop((id(active), True), None)
+            _no_device_step.add(id(active))
+            feng = None
+    eng = _engine(active, topology) if streamed and feng is None else None
     # gradient averaging, momentum 0: the fused device round, row-streamed too — each node's
     # parameter and gradient rows go up right after its backward()
-    feng = (_fused_engine(active, topology, params)
-            if not sample and _fused_ok(params) and _row_streamed(params) else None)
+    if feng is None and not sample and _fused_ok(params) and _row_streamed(params):
+        feng = _fused_engine(active, topology, params)
     if eng is None and feng is None:
         synchronize()
     if feng is not None:
@@ -639,7 +745,10 @@ def next_step(state, params, rundir):
         data, target = next(node["train-iterator"])
         # gradient averaging keeps .grad as views of the pinned gradient slab: zero in place (the
         # reference's torch 1.7.1 zero_grad behaviour) so backward accumulates into the views
-        node["optimizer"].zero_grad(set_to_none=not _averages_gradients(params))
+        if feng is not None and feng.plain:
+            feng.clear_grad_row(i)                        # -0.0: backward adds g bit for bit
+        else:
+            node["optimizer"].zero_grad(set_to_none=not _averages_gradients(params))
         loss = F.nll_loss(node["model"].forward(data, params), target)
         loss.backward()
         losses[node["rank"]] = loss.tolist()
@@ -656,12 +765,15 @@ def next_step(state, params, rundir):
             node["train-iterator"] = rest
         epoch_done[node["rank"]] = done
     defer = False
+    if weng is not None:
+        _last_round.clear()
+        _last_round[id(active)] = weng
     if not sample:
         if feng is not None:
             t0 = clock()
             feng.wait_all()
-            logging.info("  fused gradient %s + SGD step + mixing (GPU, %s, row-streamed)",
-                         feng.plan.kind, _mode(params))
+            logging.info("  gradient (%s) + SGD step + mixing (GPU, %s, row-streamed)",
+                         feng.kind, _mode(params))
             feng.run(_mode(params), defer=True)           # ★ GPU: gradient + step + mixing
             round_stats["enqueue_s"] += clock() - t0
             round_stats["rounds"] += 1

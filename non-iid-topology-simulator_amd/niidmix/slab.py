@@ -91,6 +91,12 @@ class NodeSlab:
             from .guard import tag_slab
             tag_slab(models, self)
 
+    def version(self):
+        """Sum of the parameters' in-place write counters (torch's _version): any write through the
+        parameters (an optimizer step, p.add_ / copy_ under no_grad, load_state_dict) changes it;
+        the D2H write-back and .data writes do not."""
+        return sum(q._version for slots in self._slots for _, _, q in slots)
+
     def owns(self, models):
         """True iff `models` are exactly this slab's models, in order, still backed by it (reads
         only parameter identities: no read-guard wait, niidmix.guard)."""
@@ -453,19 +459,29 @@ class ResidentRound:
     def host(self):
         return None if self.hosts is None else self.hosts[0]
 
-    def begin(self, *hosts, outs=None):
+    def begin(self, *hosts, outs=None, resident_in0=False):
         """Start a round: `hosts` are the pinned [N, P] input slabs (n_in of them), `outs` the host
-        slabs the outputs return to (default: the first n_out inputs).  Nothing is sent yet."""
+        slabs the outputs return to (default: the first n_out inputs).  Nothing is sent yet.
+
+        resident_in0: input 0 is NOT sent; the device output 0 of the last round (which holds the
+        models' current values: `fresh`) becomes this round's input 0 -- the two device buffers swap
+        roles -- and hosts[0] must be None (the device-side SGD step of the parameters)."""
         assert len(hosts) == self.n_in
+        self._enqueue_d2h(self.nblk)               # a paced write-back: the rest now (from the
+        if resident_in0:                           # output buffers as they are before the swap)
+            assert hosts[0] is None and self.fresh, "resident input 0 needs the last round's output"
+            for pt in self.parts:
+                pt["ins"][0], pt["outs"][0] = pt["outs"][0], pt["ins"][0]
         for h in hosts:
-            assert h.shape == (self.n, self.p) and h.dtype == torch.float32 and h.stride(1) == 1
+            assert h is None or (h.shape == (self.n, self.p) and h.dtype == torch.float32 and
+                                 h.stride(1) == 1)
         self.hosts = list(hosts)
-        self.hosts_out = list(outs) if outs is not None else list(hosts[:self.n_out])
-        assert len(self.hosts_out) == self.n_out
+        outs = list(outs) if outs is not None else list(hosts[:self.n_out])
+        assert len(outs) == self.n_out and all(h is not None for h in outs)
+        self.hosts_out = outs
         self.fresh = False
         self._count = [0] * self.nblk
         self._sent = [False] * self.nblk
-        self._enqueue_d2h(self.nblk)               # a paced write-back: the rest now
         for pt in self.parts:
             pt["s_h2d"].wait_stream(pt["s_d2h"])   # the host rows come back before they go up
 
@@ -482,6 +498,8 @@ class ResidentRound:
                 pt["ev_mix"] = None
             w = pt["w"]
             for h, d in zip(self.hosts, pt["ins"]):
+                if h is None:                      # resident input (begin(resident_in0=True))
+                    continue
                 _copy2d(d.data_ptr() + r0 * w * 4, w * 4,
                         h.data_ptr() + (r0 * h.stride(0) + pt["c0"]) * 4, h.stride(0) * 4, w * 4,
                         rows, 0, s)
@@ -603,7 +621,8 @@ def mixing_op(dev, part, mixer):
 def fused_op(dev, part, grad_op, step_rows, lr, mixer, grad_writeback=True):
     """ResidentRound device op of the round with gradient averaging (FusedRoundRunner's per-window
     arithmetic on the whole stripe): ins = [params, grads] -> averaged gradients (outs[1]) -> SGD
-    step of the stepped rows on the parameters in place -> mixing into outs[0]."""
+    step of the stepped rows on the parameters in place -> mixing into outs[0].  grad_op None: the
+    plain round's device step (each node's own gradient, d_sgd.py:51-52), no averaging."""
     from . import ops
     part["mixer"] = mixer
     rows = torch.as_tensor(step_rows, dtype=torch.int32).to(dev)
@@ -611,13 +630,16 @@ def fused_op(dev, part, grad_op, step_rows, lr, mixer, grad_writeback=True):
 
     def op(ins, outs, mode, kernel):
         xp, xg = ins
-        if len(outs) > 1:
+        if grad_op is None:
+            gm = xg
+        elif len(outs) > 1:
             gm = outs[1]
         else:                                 # no write-back of the averaged gradients
             if "dm" not in part:
                 part["dm"] = torch.empty_like(xg)
             gm = part["dm"]
-        grad_op(xg, out=gm)
+        if grad_op is not None:
+            grad_op(xg, out=gm)
         if rows.numel():
             ops.sgd_step_rows(xp, gm, rows, neg_lr)
         part["mixer"](xp, out=outs[0], mode=mode, kernel=kernel)

@@ -215,7 +215,7 @@ def test_training_rounds_deferred_writeback(resident, gpu, oracle_mod, monkeypat
             state, _, _ = d_sgd.init(nodes, topo, params)
             for _ in range(7):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
-                eng = d_sgd._engines.get(id(nodes))
+                eng = d_sgd.round_engine(nodes)
                 pend.append(bool(eng is not None and eng.resident is not None and
                                  eng.resident.pending))
                 if not sync_each:
@@ -316,7 +316,7 @@ def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
             state, _, _ = d_sgd.init(nodes, topo, params)
             for k in range(rounds):
                 state, _, _, _ = d_sgd.next_step(state, params, None)
-                eng = d_sgd._engines.get(id(nodes))
+                eng = d_sgd.round_engine(nodes)
                 pend.append(bool(eng is not None and eng.resident is not None and
                                  eng.resident.pending))
                 # the unpredicted reader, right after next_step: one entry point per round
@@ -366,6 +366,82 @@ def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
     stale, pend = run("gpu", False)
     assert all(pend)
     assert any(not torch.equal(u, v) for u, v in zip(stale, ref))
+
+
+@pytest.mark.parametrize("step", ["device", "cpu"])
+def test_training_rounds_device_step(step, gpu, oracle_mod, monkeypatch):
+    """the plain round with its optimizer step on the device (_FusedEngine(plain):
+    gradient rows go up after each backward, filled with -0.0 first so that backward's in-place
+    accumulate keeps every gradient's bits; p += (-lr) g on the resident parameters; mixing).  16
+    nodes, 7 rounds, with -0.0 weights and inputs whose zero pixels make +-0 gradients (where a +0
+    fill would differ): every round bitwise the reference loop (CPU SGD, then the reference mixing
+    loop).  The parameters stay on the device between rounds -- uploaded only in the first round,
+    after a guarded write (load_state_dict, round 3) and after an in-place write through a
+    parameter (p.add_ under no_grad, round 5; its version counter).  step=cpu: NIIDMIX_DEVICE_STEP=0
+    (the CPU steps; rows go up after optimizer.step())."""
+    from niidmix import d_sgd
+    monkeypatch.setenv("NIIDMIX_DEVICE_STEP", "1" if step == "device" else "0")
+    monkeypatch.setenv("NIIDMIX_ROW_BLOCK", "3")
+    n = 16
+
+    def run(mix):
+        torch.manual_seed(1337)
+        params = {"meta": {"log": "WARNING", "seed": 1337}, "model": {"input-size": 784},
+                  "topology": {"name": "ring"},
+                  "logger": {"accuracy-logging-interval": 0, "accuracy-logging-interval-steps": 0,
+                             "log-consensus-distance": False},
+                  "algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0, "batch-size": 25,
+                                "initial-averaging": False, "clique-gradient": False,
+                                "unbiased-gradient": False, "deferred-writeback": True}}
+        g = torch.Generator().manual_seed(8)
+        data = []
+        for _ in range(n * 200):
+            img = torch.rand(1, 28, 28, generator=g)
+            img[:, :, :6] = 0.0                       # zero pixels: +-0 weight gradients
+            data.append((img, int(torch.randint(0, 10, (1,), generator=g))))
+        nodes = []
+        for r in range(n):
+            mdl = RingNet()
+            with torch.no_grad():
+                mdl.fc.weight[:, :40] = -0.0          # -0.0 parameters on the zero pixels' columns
+                mdl.fc.bias[r % 10] = -0.0
+            nodes.append({"rank": r, "epoch": 0, "train-set": data[r * 200:(r + 1) * 200],
+                          "model": mdl, "optimizer": d_sgd.optimizer(mdl, params)})
+        edges = {r: [(r + 1) % n, (r - 1) % n] for r in range(n)}
+        from niidmix.topology import mh_csr
+        topo = {"edges": edges, "weights": torch.from_numpy(mh_csr(n, edges).dense())}
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False
+        snaps, eng = [], None
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for k in range(7):
+                if k == 3:
+                    nodes[5]["model"].load_state_dict(nodes[5]["model"].state_dict())
+                if k == 5:
+                    with torch.no_grad():
+                        nodes[2]["model"].fc.bias.add_(0.5)
+                state, _, _, _ = d_sgd.next_step(state, params, None)
+                eng = d_sgd.round_engine(nodes) if mix == "gpu" else None
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+        return snaps, eng
+
+    a, eng = run("gpu")
+    b, _ = run("oracle")
+    assert any((torch.signbit(u) & (u == 0)).any() for u in b)   # -0.0 survives in the reference
+    for k, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u.view(torch.int32), v.view(torch.int32)), k
+    if step == "device":
+        assert getattr(eng, "plain", False) and eng.param_uploads == 3, eng.param_uploads
+    else:
+        assert not getattr(eng, "plain", False)
 
 
 @pytest.mark.parametrize("alg",["clique", "unbiased"])
@@ -434,7 +510,7 @@ def test_training_rounds_gradient_averaging(alg, gpu, oracle_mod, monkeypatch):
             pend = []
             for _ in range(5):
                 state, losses, done, active = d_sgd.next_step(state, params, None)
-                eng = d_sgd._fused_engines.get(id(nodes))
+                eng = d_sgd.round_engine(nodes)
                 pend.append(bool(eng is not None and eng.resident is not None and
                                  eng.resident.pending))
             d_sgd.synchronize()
@@ -844,7 +920,7 @@ def test_consensus_event_in_training_rounds(gpu, monkeypatch, tmp_path):
     for _ in range(4):
         state, _, done, _ = d_sgd.next_step(state, params, None)
         if all(done.values()):
-            eng = d_sgd._engines[id(nodes)]
+            eng = d_sgd.round_engine(nodes)
             assert not eng.resident.pending                  # predicted: returned synchronised
             log.log_consensus_distance(state)
             assert nl.last_source["consensus"] == "resident"
