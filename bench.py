@@ -96,6 +96,11 @@ def parse():
                     help="also time the drop-in's WHOLE round (d_sgd.next_step: CPU training of every "
                          "node, optimizer steps, mixing) with and without the mixing, and report the "
                          "mixing's exposed cost per round (row-streamed / windowed)")
+    ap.add_argument("--e2e-rounds", type=int, default=5,
+                    help="--e2e-step: timed rounds per variant (after one warm-up round)")
+    ap.add_argument("--e2e-variants", type=str, default="",
+                    help="--e2e-step: comma-separated subset of the variants (cpu_only_slab, the "
+                         "baseline, is always run)")
     ap.add_argument("--e2e-threads", type=int, default=0,
                     help="--e2e-step: torch CPU threads for the training (default: torch's own count)")
     ap.add_argument("--layout", default="blocked", choices=["blocked", "blocked-rank", "rowmajor"],
@@ -319,7 +324,7 @@ def e2e_fused_rounds(grad_op, plan, csr, cliques, n, p, dev, rounds=3):
     return res
 
 
-def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
+def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact", only=None):
     """The drop-in's whole round, d_sgd.next_step (d_sgd.py:178-254) on the same topology: N nodes
     training on the CPU (synthetic data, a Linear(1023, 1024) model = 2^20 fp32 parameters, batch
     16), each node's optimizer.step(), then the mixing.  Variants, all built first and then run
@@ -329,8 +334,12 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
       cpu_only_slab       the same with the parameters in the drop-in's pinned host slab (the
                           baseline exposed_ms is taken against: that memory alone changes the
                           CPU's training speed on some hosts);
-      row_streamed        the plugin's default: rows go H2D right after their optimizer.step(),
-                          the mixed rows come back while the next round trains (deferred write-back);
+      row_streamed        the plugin's default: the optimizer step on the device (round 6:
+                          each node's gradient row goes H2D right after its backward(), the
+                          parameters stay resident in HBM between rounds), the mixed rows come
+                          back while the next round trains (deferred write-back);
+      row_streamed_cpu_step  the round-4/5 default: the CPU steps, parameter rows go H2D right
+                          after their optimizer.step() (NIIDMIX_DEVICE_STEP=0);
       row_streamed_paced  the same with the write-back paced (NIIDMIX_D2H_PACE=8: row blocks go D2H
                           8 ahead of the training that needs them, not all at once);
       row_streamed_sync   the same, but next_step waits for every mixed row before returning;
@@ -359,10 +368,12 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         def forward(self, x, params):
             return torch.nn.functional.log_softmax(self.fc(x), dim=1)
 
-    variants = ["cpu_only", "cpu_only_slab", "row_streamed", "row_streamed_paced",
-                "row_streamed_sync", "windowed"]
+    variants = ["cpu_only", "cpu_only_slab", "row_streamed", "row_streamed_cpu_step",
+                "row_streamed_paced", "row_streamed_sync", "windowed"]
     if cliques:
         variants += ["fused_row_streamed", "fused_windowed"]
+    if only:
+        variants = [v for v in variants if v in only or v.startswith("cpu_only")]
     orig, orig_rs = d_sgd.average, d_sgd._row_streamed
     env_res = os.environ.get("NIIDMIX_RESIDENT")
 
@@ -375,6 +386,7 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
                                 "initial-averaging": False, "clique-gradient": fused,
                                 "unbiased-gradient": False, "mixing-mode": mode,
                                 "deferred-writeback": v in ("row_streamed", "row_streamed_paced",
+                                                            "row_streamed_cpu_step",
                                                             "fused_row_streamed")}}
         torch.manual_seed(3)
         nodes = []
@@ -400,6 +412,9 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
         pace_env = os.environ.pop("NIIDMIX_D2H_PACE", None)
         if v == "row_streamed_paced":
             os.environ["NIIDMIX_D2H_PACE"] = "8"
+        step_env = os.environ.pop("NIIDMIX_DEVICE_STEP", None)
+        if v == "row_streamed_cpu_step":
+            os.environ["NIIDMIX_DEVICE_STEP"] = "0"
         try:
             for key in ("wait_s", "enqueue_s"):
                 d_sgd.round_stats[key] = 0.0
@@ -418,6 +433,9 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             os.environ.pop("NIIDMIX_D2H_PACE", None)
             if pace_env is not None:
                 os.environ["NIIDMIX_D2H_PACE"] = pace_env
+            os.environ.pop("NIIDMIX_DEVICE_STEP", None)
+            if step_env is not None:
+                os.environ["NIIDMIX_DEVICE_STEP"] = step_env
             if env_res is None:
                 os.environ.pop("NIIDMIX_RESIDENT", None)
             else:
@@ -448,7 +466,8 @@ def e2e_next_step(csr, cliques, dev, rounds=5, mode="exact"):
             out["host_blocked_ms"] = round(st["blocked"] / rounds * 1e3, 2)
             out["host_wait_ms"] = round(st["wait"] / rounds * 1e3, 2)
         res[v] = out
-    res["logger"] = e2e_logger_costs([nd["model"] for nd in sts["row_streamed"]["nodes"]])
+    if "row_streamed" in sts:
+        res["logger"] = e2e_logger_costs([nd["model"] for nd in sts["row_streamed"]["nodes"]])
     d_sgd._engines.clear()
     d_sgd._fused_engines.clear()
     del sts
@@ -1157,7 +1176,9 @@ def main():
             e2e = dict(e2e or {})
             if args.e2e_threads > 0:
                 torch.set_num_threads(args.e2e_threads)
-            e2e["next_step"] = e2e_next_step(csr, cliques, dev)
+            e2e["next_step"] = e2e_next_step(
+                csr, cliques, dev, rounds=args.e2e_rounds,
+                only=set(v for v in args.e2e_variants.split(",") if v) or None)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config != "dcliques10000":
             if args.workload == "grad-clique":
