@@ -260,7 +260,6 @@ class _FusedEngine:
         wb = not plain and os.environ.get("NIIDMIX_GRAD_WRITEBACK", "1") != "0"
         self.resident = None
         self.runner = None
-        self._ver = None
         self.param_uploads = 0          # rounds whose parameters went H2D (tests)
         if _resident_ok() and ResidentRound.fits(n, p, devices, buffers=4 if wb else 3):
             self.resident = ResidentRound(
@@ -269,6 +268,7 @@ class _FusedEngine:
                                            self.mixer if dev == devices[0] else self.mixer.to(dev)),
                 n, p, devices, block=_row_block(), n_in=2, n_out=2 if wb else 1)
             self.outs = (self.slab.host, self.gslab.host) if wb else (self.slab.host,)
+            self.resident.version_of = self.slab.version
             guard.install(models, self.resident)
         elif not plain:
             def make(dev, n, cols):
@@ -285,9 +285,7 @@ class _FusedEngine:
         """The device holds the models' current parameters: the last round's mixed output, with no
         write to the models since (guarded writes clear `fresh`; the version counters catch writes
         through the parameters, e.g. an optimizer step or p.add_ under no_grad)."""
-        rr = self.resident
-        return (rr is not None and rr.fresh and self._ver is not None
-                and self.slab.version() == self._ver)
+        return self.resident is not None and self.resident.current()
 
     def clear_grad_row(self, i):
         """Before node i's backward: its gradient views to -0.0 (see the class docstring)."""
@@ -319,7 +317,6 @@ class _FusedEngine:
             if self.resident.hosts is None:
                 self.begin_round()                    # nothing streamed: every row goes up now
             self.resident.mix(mode, timing=timing)
-            self._ver = self.slab.version()
             if not defer:
                 self.resident.wait_all()
                 return self.resident.last_timing
@@ -430,6 +427,7 @@ class _Engine:
                 lambda dev, part: mixing_op(dev, part, self.mixer if dev == devices[0]
                                             else self.mixer.to(dev)),
                 n, p, devices, block=_row_block())
+            self.resident.version_of = self.slab.version
             guard.install(self.slab.models, self.resident)
         else:
             self.runner = MultiDeviceRound(
@@ -511,6 +509,16 @@ def _mode(params):
     if mode not in ("exact", "fast"):
         raise ValueError(f"unknown mixing mode {mode!r}")
     return mode
+
+
+def invalidate(nodes=None):
+    """Declare the models of `nodes` (default: every node list) written behind the plugin's back
+    (p.data.copy_, a raw pointer): the next round uploads their parameters again and the logger
+    hooks stop reading the device copy."""
+    for eng in list(_engines.values()) + list(_fused_engines.values()):
+        rr = getattr(eng, "resident", None)
+        if rr is not None and (nodes is None or eng.slab.owns([n["model"] for n in nodes])):
+            rr.fresh = False
 
 
 def round_engine(nodes):

@@ -50,7 +50,7 @@ def _fresh_resident(models):
     if hit is None:
         return None
     rr, rows = hit
-    if not getattr(rr, "fresh", False) or not hasattr(rr, "parts"):
+    if not hasattr(rr, "parts") or not rr.current():
         return None
     return rr, rows
 

@@ -441,7 +441,14 @@ class ResidentRound:
         self._pace = 0
         # the device outputs (outs[0]: the mixed parameters) hold the models' current values: set
         # by mix(), cleared by begin() and by guarded writes (niidmix.guard); read by niidmix.logger
+        # and the device-step round through current(), which also compares the models' version
+        # counters (version_of: NodeSlab.version) with their value at mix() -- an in-place write
+        # through a parameter (p.add_ under no_grad, an optimizer step) is caught there.  Writes
+        # that bypass both (p.data.copy_, a raw pointer) are not: call
+        # niidmix.d_sgd.invalidate(nodes) after such a write.
         self.fresh = False
+        self.version_of = None
+        self.models_version = None
         self.last_timing = None
 
     @staticmethod
@@ -469,7 +476,8 @@ class ResidentRound:
         assert len(hosts) == self.n_in
         self._enqueue_d2h(self.nblk)               # a paced write-back: the rest now (from the
         if resident_in0:                           # output buffers as they are before the swap)
-            assert hosts[0] is None and self.fresh, "resident input 0 needs the last round's output"
+            assert hosts[0] is None and self.current(), \
+                "resident input 0 needs the last round's output"
             for pt in self.parts:
                 pt["ins"][0], pt["outs"][0] = pt["outs"][0], pt["ins"][0]
         for h in hosts:
@@ -557,6 +565,7 @@ class ResidentRound:
         self._enqueue_d2h(self.nblk if pace <= 0 else min(self.nblk, pace))
         self._pace = pace
         self.fresh = True
+        self.models_version = self.version_of() if self.version_of is not None else None
         self.hosts = None                           # row_ready() is a no-op until begin()
         self._timing = (timing, t0, t_ev, unsent)
 
@@ -606,6 +615,10 @@ class ResidentRound:
     @property
     def pending(self):
         return self._done is not None
+
+    def current(self):
+        """The device outputs still hold the models' current values (see `fresh`)."""
+        return self.fresh and (self.version_of is None or self.version_of() == self.models_version)
 
 
 def mixing_op(dev, part, mixer):

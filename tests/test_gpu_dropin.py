@@ -869,6 +869,15 @@ def test_logger_hooks_read_resident_slab(gpu, monkeypatch, tmp_path):
         flat = torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy()
         assert oracle_bitwise(flat, g[key]), key
         assert guard.row_tag(c) is None and type(c) is FlatModel     # a plain copy
+    # an in-place write through a parameter (no Module method: the guard does not
+    # see it) bumps the version counter, so the device copy is no longer trusted
+    with torch.no_grad():
+        models[4].ps[0].mul_(1.0)
+    assert eng.resident.fresh and not eng.resident.current()
+    c = sm.average(models)
+    assert nl.last_source["average"] == "stacked"           # (values unchanged: x * 1.0)
+    assert oracle_bitwise(torch.cat([q.detach().reshape(-1) for q in c.parameters()]).numpy(),
+                          g["center_all"])
     # a guarded write (load_state_dict) makes the device copy stale: the next read stacks
     models[5].load_state_dict(models[5].state_dict())
     assert not eng.resident.fresh

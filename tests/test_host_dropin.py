@@ -227,10 +227,14 @@ def test_slab_models_pickle_compact():
     buf = io.BytesIO()
     torch.save(m, buf)
     assert buf.tell() < 2 * one + 4096
+    v0 = slab.version()
     with torch.no_grad():
         m.bias.add_(1.0)
     assert torch.equal(slab.host[17, 1000:], m.bias.detach())
     assert slab.owns(models)
+    assert slab.version() == v0 + 1          # in-place writes through a parameter are counted
+    slab.host[3].fill_(0.5)                  # raw slab writes (the D2H write-back) are not
+    assert slab.version() == v0 + 1
 
 
 def test_guarded_model_pickles_as_base_class(monkeypatch):
