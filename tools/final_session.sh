@@ -1,13 +1,14 @@
 #!/bin/bash
-# Closing GPU session of a round (run through gpurun with the final library): the GPU test suite,
+# Closing GPU session of a round (through gpurun, with the final library; round 6 layout): the GPU test suite,
 # smoke, the headline bench line, then per bench config a bench line, a kernel trace (--stats) and
 # two separate PMC passes (FETCH_SIZE, WRITE_SIZE) whose per-launch bytes are stamped with the
-# library hash into $O/traffic.json (a copy of profiles/traffic.json, copied back by hand).
+# library hash into $O/traffic.json (a copy of profiles/traffic.json, copied back by hand), then
+# the whole-round E2E.  Every GPU step has its own time limit; a step that fails ends the session.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"
 O=gpurun_out/${1:-final}; mkdir -p $O; export TMPDIR=/tmp
 cp profiles/traffic.json $O/traffic.json
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -rs --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log; grep -E "FAILED" $O/pytest_gpu.log | head
 [ $rc -ge 2 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; cat $O/smoke.log; exit 3; }
@@ -17,9 +18,9 @@ cat $O/bench_headline_default.json
 one() {   # name kernel-substring alg-bytes bench-args...
   n=$1; k=$2; alg=$3; shift 3
   timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench $n failed"; tail -5 $O/bench_$n.err; return 1; }
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt_$n -o kt -- python3 $R/bench.py --no-cpu-baseline "$@" > $O/kt_$n.log 2>&1 || { echo "trace $n failed"; tail -5 $O/kt_$n.log; return 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt_$n -o kt -- python3 $R/bench.py --no-cpu-baseline --no-cold-cache "$@" > $O/kt_$n.log 2>&1 || { echo "trace $n failed"; tail -5 $O/kt_$n.log; return 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/$O/pmc_${n}_$c -o p -- python3 $R/bench.py --no-cpu-baseline "$@" > $O/pmc_${n}_$c.log 2>&1 || { echo "pmc $n $c failed"; tail -5 $O/pmc_${n}_$c.log; return 1; }
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/$O/pmc_${n}_$c -o p -- python3 $R/bench.py --no-cpu-baseline --no-cold-cache "$@" > $O/pmc_${n}_$c.log 2>&1 || { echo "pmc $n $c failed"; tail -5 $O/pmc_${n}_$c.log; return 1; }
   done
   python tools/pmc_traffic.py $O/pmc_${n}_FETCH_SIZE $O/pmc_${n}_WRITE_SIZE $k --alg-bytes $alg --key-from $O/bench_$n.json --out $O/traffic.json > $O/traffic_$n.txt || return 1
   python -c "import json;d=json.load(open('$O/bench_$n.json'));t=json.load(open('$O/traffic_$n.txt'));print('$n', d['ms_per_step'], 'ms', d['roofline']['frac'], 'traffic x', round(t['ratio_to_algorithmic'],4))"
@@ -28,9 +29,11 @@ one headline k_mix_clique 8388608000 --steps 20 || exit 5
 one exact k_mix_tile_lds 8388608000 --kernel tile-lds-exact --steps 10 || exit 5
 one fc1000 k_mix_bigclique 8388608000 --config fc1000 --steps 10 || exit 5
 one d10k k_mix_clique 83886080000 --config dcliques10000 --steps 5 --warmup 2 || exit 5
-one ring100 k_mix_ell 49604800 --config ring100 --steps 200 || exit 5
+one d10k_exact k_mix_tile_lds 83886080000 --config dcliques10000 --kernel tile-lds-exact --steps 3 --warmup 1 || exit 5
+one ring100 k_mix_strip 49604800 --config ring100 --steps 200 || exit 5
 one grad k_grad_segment_mean 8388608000 --workload grad-clique --steps 10 || exit 5
-one dense k_mix_dense 8388608000 --config fc1000 --kernel dense --steps 3 --warmup 1 || exit 5
-timeout -k 10 600 python bench.py --no-cpu-baseline --e2e --steps 3 > $O/bench_e2e.json 2> $O/bench_e2e.err || { echo e2e failed; tail $O/bench_e2e.err; exit 6; }
-python -c "import json;d=json.load(open('$O/bench_e2e.json'));print(d.get('e2e'))"
+one dense k_mix_dense_b6 8388608000 --config fc1000 --kernel dense --steps 5 --warmup 2 || exit 5
+one dense_f32 "k_mix_dense<" 8388608000 --config fc1000 --kernel dense-f32 --steps 3 --warmup 1 || exit 5
+timeout -k 10 900 python bench.py --no-cpu-baseline --e2e --e2e-step --steps 3 > $O/bench_e2e.json 2> $O/bench_e2e.err || { echo e2e failed; tail $O/bench_e2e.err; exit 6; }
+python -c "import json;d=json.load(open('$O/bench_e2e.json'));print(json.dumps(d.get('e2e')))"
 echo done
