@@ -1719,6 +1719,218 @@ __global__ __launch_bounds__(256, 1) void k_mix_dense_b6w(
     }
 }
 
+// The same GEMM with the W tiles staged by LDS-DMA (round 6; NIIDMIX_DENSE_B6_DMA).
+// The pre-split W pieces go straight from memory into LDS (buffer_load_dwordx4 ... lds: lane l of
+// a wave-instruction writes 16 B at M0 + 16 l), so no W piece occupies VGPRs or costs a ds_write,
+// and the W fetch of step s + NA - 1 goes out at the top of step s into an NA-deep ring of LDS
+// buffers (NA 3: two K-steps ahead, as the X values; NA 2: one).  The A layout and its half swizzle
+// are those of k_mix_dense_b6: the DMA's lane order fixes WHERE a piece lands, so each lane loads
+// the piece that belongs at its slot.  X is fetched into registers two steps ahead and split into
+// the double-buffered B planes as before.  The block barrier is an inline-asm s_barrier preceded by
+// an explicit s_waitcnt that waits for this wave's W DMA of the next step only (the compiler's
+// __syncthreads() drains vmcnt(0) once an LDS-DMA is in flight, which would also wait for the X
+// fetch issued two steps ahead).  WN 2 (4 waves of 128 x 64 per 256 x 128 tile) with NA 2 fits two
+// blocks per CU, whose barriers are independent: the two waves of a SIMD then belong to different
+// blocks.  Products, K order and MFMA per output element are those of k_mix_dense_b6: bit-identical.
+#define B6D_STR2(x) #x
+#define B6D_STR(x) B6D_STR2(x)
+template <int WN, int TM, int NA>
+__global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
+    int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
+    int64_t n_items, const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
+    const float *__restrict__ csr_val) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    constexpr int NW = 2 * WN;                             // waves
+    constexpr int BN = 64 * WN;                            // columns per block tile
+    constexpr int BM = 64 * TM;                            // rows per block tile
+    constexpr int ABUF = 3 * BM * 2;                       // 16-B W pieces per K-step (A buffer)
+    constexpr int NDMA = ABUF / 64;                        // wave-level DMAs per K-step
+    static_assert(NDMA % NW == 0, "DMAs per wave");
+    constexpr int DPW = NDMA / NW;                         // DMAs per wave per K-step
+    static_assert(NA == 2 || NA == 3, "A ring depth");
+    extern __shared__ uint4 lds_b6[];
+    auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
+        return lds_b6[((b * 3 + pl) * BM + row) * 2 + hf];
+    };
+    auto B_at = [&](int b, int pl, int col, int hf) -> uint4 & {
+        return lds_b6[NA * ABUF + ((b * 3 + pl) * BN + col) * 2 + hf];
+    };
+    const int tid = threadIdx.x;
+    const int wave = wave_id();
+    const int lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int bj = tid % BN, bh = tid / BN;                // X loader: column, k half
+    const int hl = lane >> 5;
+    const int64_t S = kpad / kB6K;
+    const int64_t plane_el = mpad * kpad;
+    // this lane's piece of each of its wave's DMAs: LDS slot q = 64 j + lane of the A buffer holds
+    // plane pl, row, stored half hs; the piece there is W half hf = hs ^ (row >> 3 & 1)
+    uint32_t wrel[DPW];
+#pragma unroll
+    for (int u = 0; u < DPW; ++u) {
+        const int q = 64 * (wave + NW * u) + lane;
+        const int pl = q / (2 * BM), rem = q % (2 * BM);
+        const int row = rem >> 1, hf = (rem & 1) ^ ((row >> 3) & 1);
+        wrel[u] = (uint32_t)((((int64_t)pl * mpad + row) * kpad + 8 * hf) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(wp), (short)0, (int)(3 * plane_el * 2), 0x00020000);
+    const uint32_t rowb = (uint32_t)ld_x * 4u;
+    const int bhu = __builtin_amdgcn_readfirstlane(bh);
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int64_t jt = (local / n_it) * 8 + xcd;
+        const int64_t it = local % n_it;
+        const int64_t i0 = it * BM, j0 = jt * BN;
+        if (j0 >= p) continue;                             // block-uniform
+        floatx16 acc[TM][2];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        const int64_t jx = j0 + bj;
+        const uint32_t xvoff = jx < p ? (uint32_t)jx * 4u : 0x80000000u;
+        uint32_t wvoff[DPW];
+#pragma unroll
+        for (int u = 0; u < DPW; ++u) wvoff[u] = wrel[u] + (uint32_t)(i0 * kpad * 2);
+        float xv0[8], xv1[8];
+        // W pieces of K-step S_ (clamped) into A buffer AB_ by this wave's DPW DMAs
+#define B6D_WDMA(AB_, S_)                                                                          \
+        do {                                                                                       \
+            const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
+            _Pragma("unroll") for (int u = 0; u < DPW; ++u)                                        \
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(                                          \
+                    wrs, (lds_void *)(lds_b6 + (AB_) * ABUF + 64 * (wave + NW * u)), 16, wvoff[u], \
+                    (int)(k0_ * 2), 0, 0);                                                         \
+        } while (0)
+#define B6D_XFETCH(SET, S_)                                                                        \
+        do {                                                                                       \
+            const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
+            const int64_t ext_ = (n - k0_) * (int64_t)rowb;                                        \
+            const __amdgpu_buffer_rsrc_t xr_ = __builtin_amdgcn_make_buffer_rsrc(                  \
+                const_cast<float *>(x + k0_ * ld_x), (short)0,                                     \
+                (int)(ext_ < 0x7fffffffLL ? ext_ : 0x7fffffffLL), 0x00020000);                     \
+            _Pragma("unroll") for (int u = 0; u < 8; ++u)                                          \
+                xv##SET[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(       \
+                                 xr_, xvoff, (int)((8 * bhu + u) * rowb), 0));                     \
+        } while (0)
+        // the planes go to LDS by inline-asm ds_write_b128: hipcc, which cannot tell them from
+        // the W ring's LDS-DMA destinations, would otherwise wait for the DMA of step s + NA - 1
+        // (vmcnt) before each write; the barrier's explicit lgkmcnt(0) covers them
+        typedef unsigned b6d_u32x4 __attribute__((ext_vector_type(4)));
+        const uint32_t bst = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint4 *)lds_b6) +
+                             (uint32_t)(NA * ABUF + bj * 2 + (bh ^ ((bj >> 3) & 1))) * 16u;
+#define B6D_XSTASH(SET, BUF)                                                                       \
+        do {                                                                                       \
+            uint32_t h_[4], m_[4], l_[4];                                                          \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u)                                          \
+                split3_pair(xv##SET[2 * u], xv##SET[2 * u + 1], h_[u], m_[u], l_[u]);              \
+            const b6d_u32x4 hv_ = {h_[0], h_[1], h_[2], h_[3]}, mv_ = {m_[0], m_[1], m_[2], m_[3]}, \
+                            lv_ = {l_[0], l_[1], l_[2], l_[3]};                                    \
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(bst), "v"(hv_),                   \
+                         "n"(((BUF) * 3 + 0) * BN * 32) : "memory");                               \
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(bst), "v"(mv_),                   \
+                         "n"(((BUF) * 3 + 1) * BN * 32) : "memory");                               \
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(bst), "v"(lv_),                   \
+                         "n"(((BUF) * 3 + 2) * BN * 32) : "memory");                               \
+        } while (0)
+        // the barrier: this wave's DMA of the next K-step has landed (everything issued after it --
+        // the X loads of step s + 2, and with NA 3 the DMA of step s + 2 -- may stay in flight),
+        // and its LDS reads and writes are done
+#define B6D_VMAFTER (NA == 3 ? DPW + 8 : 8)
+#define B6D_BARRIER()                                                                              \
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(B6D_VMAFTER) : "memory")
+        // K-step s: A buffer AB (runtime ring index), B buffer B, X register set B; the W DMA of
+        // s + NA - 1 into ring slot AN and the X fetch of s + 2 first, then the operand reads, the
+        // MFMAs, the split of s + 1 into B buffer NB, the barrier
+#define B6D_STEP(B, NB, S_, AB, AN)                                                                \
+        do {                                                                                       \
+            B6D_WDMA(AN, (S_) + NA - 1);                                                           \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            B6D_XFETCH(B, (S_) + 2);                                                               \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            bf16x8v af_[TM][3], bf_[2][3];                                                          \
+            _Pragma("unroll") for (int o = 0; o < 3; ++o) {                                        \
+                const int pa_ = o == 0 ? 1 : o == 1 ? 2 : 0, pb_ = o == 0 ? 1 : o == 1 ? 0 : 2;    \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a) {                                   \
+                    const int row_ = wm * 32 * TM + a * 32 + (lane & 31);                          \
+                    af_[a][pa_] = __builtin_bit_cast(bf16x8v, A_at(AB, pa_, row_, hl ^ ((row_ >> 3) & 1))); \
+                }                                                                                  \
+                _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                    \
+                    const int col_ = wn * 64 + c * 32 + (lane & 31);                               \
+                    bf_[c][pb_] = __builtin_bit_cast(bf16x8v, B_at(B, pb_, col_, hl ^ ((col_ >> 3) & 1))); \
+                }                                                                                  \
+            }                                                                                      \
+            _Pragma("unroll") for (int e = 0; e < 6; ++e)                                          \
+                _Pragma("unroll") for (int a = 0; a < TM; ++a)                                     \
+                    _Pragma("unroll") for (int c = 0; c < 2; ++c)                                  \
+                        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
+                            af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
+            B6D_XSTASH(NB, NB);                                                                    \
+            B6D_BARRIER();                                                                         \
+        } while (0)
+        // prologue: W of steps 0 .. NA - 2, X of steps 0 and 1, X 0 split into B buffer 0
+#pragma unroll
+        for (int a = 0; a < NA - 1; ++a) B6D_WDMA(a, a);
+        __builtin_amdgcn_sched_barrier(0);
+        B6D_XFETCH(0, 0);
+        B6D_XFETCH(1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        B6D_XSTASH(0, 0);
+        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int ab = 0;                                        // ring slot of step s
+        int64_t s = 0;
+        for (; s + 1 < S; s += 2) {
+            const int a1 = ab + 1 == NA ? 0 : ab + 1;
+            const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;       // (s + NA - 1) % NA
+            const int an1 = an0 + 1 == NA ? 0 : an0 + 1;
+            B6D_STEP(0, 1, s, ab, an0);
+            B6D_STEP(1, 0, s + 1, a1, an1);
+            ab = a1 + 1 == NA ? 0 : a1 + 1;
+        }
+        if (s < S) {
+            const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;
+            B6D_STEP(0, 1, s, ab, an0);
+        }
+#undef B6D_STEP
+#undef B6D_BARRIER
+#undef B6D_VMAFTER
+#undef B6D_XSTASH
+#undef B6D_XFETCH
+#undef B6D_WDMA
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped refetches past the end
+        uint64_t bad[2] = {0, 0};                          // this lane's non-finite outputs
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t i = i0 + wm * 32 * TM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
+                    if (i < n && j < p) {
+                        if (__builtin_isfinite(acc[a][c][r])) __builtin_nontemporal_store(acc[a][c][r], y + i * ld_y + j);
+                        else bad[a >> 1] |= 1ull << ((a & 1) * 32 + c * 16 + r);
+                    }
+                }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            while (bad[h]) {                               // non-finite guard (csr_refix1)
+                const int q = __builtin_ctzll(bad[h]);
+                bad[h] &= bad[h] - 1;
+                const int a = 2 * h + (q >> 5), c = (q >> 4) & 1, r = q & 15;
+                const int64_t i = i0 + wm * 32 * TM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int64_t j = j0 + wn * 64 + c * 32 + (lane & 31);
+                __builtin_nontemporal_store(csr_refix1(x + j, ld_x, i, csr_ptr, csr_col, csr_val), y + i * ld_y + j);
+            }
+        __syncthreads();   // LDS buffers are rewritten by the next item's prologue
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // Clique-factored mixing for BIG cliques (> 256 members, e.g. a fully-connected topology with MH
 // weights = one clique: W = a*I + c*11^T).  Work item = (clique, 64 columns), WAVES waves, lane =
@@ -4452,6 +4664,29 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
         hipLaunchKernelGGL((k_mix_dense_b6<WN, SC, AB, TM>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
+    // W tiles by LDS-DMA (k_mix_dense_b6d): NIIDMIX_DENSE_B6_DMA = "WN,NA" -- 4,3 (256 x 256, one
+    // block per CU, W two K-steps ahead), 4,2, or 2,2 (256 x 128, two blocks per CU)
+    if (const char *e = getenv("NIIDMIX_DENSE_B6_DMA")) {
+        int dwn = 0, dna = 0;
+        if (sscanf(e, "%d,%d", &dwn, &dna) == 2 && dwn != 0) {
+#define NIIDMIX_B6D(WN, NA) do { \
+            const int64_t n_it = mpad / 256, n_jt = (p + 64 * WN - 1) / (64 * WN); \
+            const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8; \
+            const size_t lds = ((size_t)NA * 3 * 256 * 2 + (size_t)2 * 3 * 64 * WN * 2) * sizeof(uint4); \
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6d<WN, 4, NA>), \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+                return set_error(NIIDMIX_EHIP, "k_mix_dense_b6d: %zu B of LDS refused", lds); \
+            hipLaunchKernelGGL((k_mix_dense_b6d<WN, 4, NA>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
+                               x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
+        } while (0)
+            if (dwn == 4 && dna == 3) NIIDMIX_B6D(4, 3);
+            else if (dwn == 4 && dna == 2) NIIDMIX_B6D(4, 2);
+            else if (dwn == 2 && dna == 2) NIIDMIX_B6D(2, 2);
+            else return set_error(NIIDMIX_EINVAL, "NIIDMIX_DENSE_B6_DMA=%s: 4,3 / 4,2 / 2,2", e);
+#undef NIIDMIX_B6D
+            return check_launch("k_mix_dense_b6d");
+        }
+    }
     // one wave per SIMD (k_mix_dense_b6w, 256 x 256 tile of 4 waves of 128 x 128): tuning A/B
     if (const char *e = getenv("NIIDMIX_DENSE_B6_W1")) if (atoi(e) == 1) {
         const int64_t n_it = mpad / 256, n_jt = (p + 255) / 256;

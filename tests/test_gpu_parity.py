@@ -836,11 +836,15 @@ def test_dense_b6_tail_rows_not_read(gpu):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), n
 
 
+@pytest.mark.parametrize("variant", [("NIIDMIX_DENSE_B6_W1", "1"), ("NIIDMIX_DENSE_B6_DMA", "4,3"),
+                                     ("NIIDMIX_DENSE_B6_DMA", "4,2"), ("NIIDMIX_DENSE_B6_DMA", "2,2")])
 @pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (257, 1030), (300, 70000)])
-def test_dense_b6_one_wave_per_simd_bitwise(n, p, gpu, monkeypatch):
-    """The one-wave-per-SIMD bf16x6 kernel (k_mix_dense_b6w, 4 waves of 128 x 128) and the
-    two-wave kernel (8 waves of 128 x 64) run the same products in the same K order through the
-    same MFMA per output element: their outputs are bit-identical, non-finite guard included."""
+def test_dense_b6_variants_bitwise(n, p, variant, gpu, monkeypatch):
+    """The bf16x6 kernel's variants run the same products in the same K order through the same
+    MFMA per output element as the default (8 waves of 128 x 64, W through registers), so their
+    outputs are bit-identical, non-finite guard included: one wave per SIMD (k_mix_dense_b6w, 4
+    waves of 128 x 128) and the W tiles by LDS-DMA (k_mix_dense_b6d, round 6: 256 x 256 with a
+    three- or two-deep W ring, and 256 x 128 blocks two per CU)."""
     ops = _ops()
     rng = np.random.default_rng(7 * n + p)
     w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)
@@ -849,11 +853,26 @@ def test_dense_b6_one_wave_per_simd_bitwise(n, p, gpu, monkeypatch):
     xn = rng.standard_normal((n, p)).astype(np.float32)
     xn[n // 2, p // 3] = np.inf                       # a non-finite input: its column is recomputed
     x = torch.from_numpy(xn).to(gpu)
-    out = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("NIIDMIX_DENSE_B6_W1", v)
-        out[v] = m(x, kernel="dense").cpu().numpy()
-    assert np.array_equal(out["0"].view(np.uint32), out["1"].view(np.uint32))
+    monkeypatch.delenv("NIIDMIX_DENSE_B6_W1", raising=False)
+    monkeypatch.delenv("NIIDMIX_DENSE_B6_DMA", raising=False)
+    base = m(x, kernel="dense").cpu().numpy()
+    monkeypatch.setenv(*variant)
+    got = m(x, kernel="dense").cpu().numpy()
+    assert np.array_equal(base.view(np.uint32), got.view(np.uint32))
+    xn2 = rng.standard_normal((n, p)).astype(np.float32) * 3
+    ref = oracle_c_tol(xn2, m, gpu)
+    assert ref
+
+
+def oracle_c_tol(xn, m, gpu):
+    """m's current dense kernel on xn within the 1e-5 condition-aware tolerance of the C oracle."""
+    from oracle import oracle
+    csr = m.csr
+    y = m(torch.from_numpy(xn).to(gpu), kernel="dense").cpu().numpy()
+    ref = oracle.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
+    bound = oracle.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
+    ok, worst = oracle.check_tolerance(y, ref, bound, rtol=RTOL)
+    return ok
 
 
 def _dense_csr(w):

@@ -12,6 +12,7 @@
 #   pmc:CTRS|ARGS    rocprofv3 --pmc CTRS (one pass) over bench.py --no-cpu-baseline ARGS -> pmc_K/
 #   py:ARGS          python ARGS (a tool or probe script)                              -> py_K.log
 #   smoke:           __graft_entry__.smoke()                                           -> smoke.log
+#   sh:CMD           bash -c CMD (env settings, A/B loops)                              -> sh_K.log
 # K is the step's index.  STEP_TIMEOUT (seconds, default 600) bounds each step.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -48,6 +49,9 @@ for step in "$@"; do
     py)
       timeout -k 10 "$T" python -u $args > "$O/py_$k.log" 2>&1
       rc=$?; tail -15 "$O/py_$k.log" ;;
+    sh)
+      timeout -k 10 "$T" bash -c "$args" > "$O/sh_$k.log" 2>&1
+      rc=$?; tail -25 "$O/sh_$k.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
       rc=$?; cat "$O/smoke.log" ;;
