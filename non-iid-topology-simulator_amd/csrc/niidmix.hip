@@ -1732,15 +1732,19 @@ __global__ __launch_bounds__(256, 1) void k_mix_dense_b6w(
 // fetch issued two steps ahead).  WN 2 (4 waves of 128 x 64 per 256 x 128 tile) with NA 2 fits two
 // blocks per CU, whose barriers are independent: the two waves of a SIMD then belong to different
 // blocks.  Products, K order and MFMA per output element are those of k_mix_dense_b6: bit-identical.
-#define B6D_STR2(x) #x
-#define B6D_STR(x) B6D_STR2(x)
-template <int WN, int TM, int NA>
+// one wave-instruction of the W ring's LDS-DMA: lane l's 16 B at voff + soff land at lds + 16 l
+__device__ __forceinline__ void b6d_dma16(__amdgpu_buffer_rsrc_t rsrc, uint4 *lds, uint32_t voff,
+                                          int soff) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void *)lds, 16, voff, soff, 0, 0);
+}
+
+template <int WN, int TM, int NA, int XD>
 __global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t n,
     int64_t p, const uint16_t *__restrict__ wp, int64_t mpad, int64_t kpad, int64_t n_it,
     int64_t n_items, const int64_t *__restrict__ csr_ptr, const int32_t *__restrict__ csr_col,
     const float *__restrict__ csr_val) {
-    typedef __attribute__((address_space(3))) void lds_void;
     constexpr int NW = 2 * WN;                             // waves
     constexpr int BN = 64 * WN;                            // columns per block tile
     constexpr int BM = 64 * TM;                            // rows per block tile
@@ -1749,6 +1753,7 @@ __global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
     static_assert(NDMA % NW == 0, "DMAs per wave");
     constexpr int DPW = NDMA / NW;                         // DMAs per wave per K-step
     static_assert(NA == 2 || NA == 3, "A ring depth");
+    static_assert(XD == 2 || (XD == 3 && NA == 2), "X prefetch distance (3: with a 2-deep W ring)");
     extern __shared__ uint4 lds_b6[];
     auto A_at = [&](int b, int pl, int row, int hf) -> uint4 & {
         return lds_b6[((b * 3 + pl) * BM + row) * 2 + hf];
@@ -1797,15 +1802,14 @@ __global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
         uint32_t wvoff[DPW];
 #pragma unroll
         for (int u = 0; u < DPW; ++u) wvoff[u] = wrel[u] + (uint32_t)(i0 * kpad * 2);
-        float xv0[8], xv1[8];
+        float xv0[8], xv1[8], xv2[8];
         // W pieces of K-step S_ (clamped) into A buffer AB_ by this wave's DPW DMAs
 #define B6D_WDMA(AB_, S_)                                                                          \
         do {                                                                                       \
             const int64_t k0_ = ((S_) < S ? (S_) : S - 1) * kB6K;                                 \
             _Pragma("unroll") for (int u = 0; u < DPW; ++u)                                        \
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(                                          \
-                    wrs, (lds_void *)(lds_b6 + (AB_) * ABUF + 64 * (wave + NW * u)), 16, wvoff[u], \
-                    (int)(k0_ * 2), 0, 0);                                                         \
+                b6d_dma16(wrs, lds_b6 + (AB_) * ABUF + 64 * (wave + NW * u), wvoff[u],             \
+                          (int)(k0_ * 2));                                                         \
         } while (0)
 #define B6D_XFETCH(SET, S_)                                                                        \
         do {                                                                                       \
@@ -1839,19 +1843,19 @@ __global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
                          "n"(((BUF) * 3 + 2) * BN * 32) : "memory");                               \
         } while (0)
         // the barrier: this wave's DMA of the next K-step has landed (everything issued after it --
-        // the X loads of step s + 2, and with NA 3 the DMA of step s + 2 -- may stay in flight),
+        // the X loads of step s + XD, and with NA 3 the DMA of step s + 2 -- may stay in flight),
         // and its LDS reads and writes are done
 #define B6D_VMAFTER (NA == 3 ? DPW + 8 : 8)
 #define B6D_BARRIER()                                                                              \
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(B6D_VMAFTER) : "memory")
-        // K-step s: A buffer AB (runtime ring index), B buffer B, X register set B; the W DMA of
-        // s + NA - 1 into ring slot AN and the X fetch of s + 2 first, then the operand reads, the
-        // MFMAs, the split of s + 1 into B buffer NB, the barrier
-#define B6D_STEP(B, NB, S_, AB, AN)                                                                \
+        // K-step s: A buffer AB (runtime ring index), B buffer B; the W DMA of s + NA - 1 into
+        // ring slot AN and the X fetch of s + XD into register set XL first, then the operand
+        // reads, the MFMAs, the split of s + 1 (register set XS) into B buffer NB, the barrier
+#define B6D_STEP(B, NB, XL, XS, S_, AB, AN)                                                        \
         do {                                                                                       \
             B6D_WDMA(AN, (S_) + NA - 1);                                                           \
             __builtin_amdgcn_sched_barrier(0);                                                     \
-            B6D_XFETCH(B, (S_) + 2);                                                               \
+            B6D_XFETCH(XL, (S_) + XD);                                                             \
             __builtin_amdgcn_sched_barrier(0);                                                     \
             bf16x8v af_[TM][3], bf_[2][3];                                                          \
             _Pragma("unroll") for (int o = 0; o < 3; ++o) {                                        \
@@ -1870,31 +1874,51 @@ __global__ __launch_bounds__(128 * WN, (WN == 2 ? 2 : 1)) void k_mix_dense_b6d(
                     _Pragma("unroll") for (int c = 0; c < 2; ++c)                                  \
                         acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                       \
                             af_[a][kB6PA[e]], bf_[c][kB6PB[e]], acc[a][c], 0, 0, 0);               \
-            B6D_XSTASH(NB, NB);                                                                    \
+            B6D_XSTASH(XS, NB);                                                                    \
             B6D_BARRIER();                                                                         \
         } while (0)
-        // prologue: W of steps 0 .. NA - 2, X of steps 0 and 1, X 0 split into B buffer 0
+        // prologue: W of steps 0 .. NA - 2, X of steps 0 .. XD - 1, X 0 split into B buffer 0
 #pragma unroll
         for (int a = 0; a < NA - 1; ++a) B6D_WDMA(a, a);
         __builtin_amdgcn_sched_barrier(0);
         B6D_XFETCH(0, 0);
         B6D_XFETCH(1, 1);
+        if (XD == 3) B6D_XFETCH(2, 2);
         __builtin_amdgcn_sched_barrier(0);
         B6D_XSTASH(0, 0);
-        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (XD == 3) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         int ab = 0;                                        // ring slot of step s
         int64_t s = 0;
-        for (; s + 1 < S; s += 2) {
-            const int a1 = ab + 1 == NA ? 0 : ab + 1;
-            const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;       // (s + NA - 1) % NA
-            const int an1 = an0 + 1 == NA ? 0 : an0 + 1;
-            B6D_STEP(0, 1, s, ab, an0);
-            B6D_STEP(1, 0, s + 1, a1, an1);
-            ab = a1 + 1 == NA ? 0 : a1 + 1;
-        }
-        if (s < S) {
-            const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;
-            B6D_STEP(0, 1, s, ab, an0);
+        if constexpr (XD == 2) {
+            for (; s + 1 < S; s += 2) {
+                const int a1 = ab + 1 == NA ? 0 : ab + 1;
+                const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;   // (s + NA - 1) % NA
+                const int an1 = an0 + 1 == NA ? 0 : an0 + 1;
+                B6D_STEP(0, 1, 0, 1, s, ab, an0);
+                B6D_STEP(1, 0, 1, 0, s + 1, a1, an1);
+                ab = a1 + 1 == NA ? 0 : a1 + 1;
+            }
+            if (s < S) {
+                const int an0 = ab + NA - 1 >= NA ? ab - 1 : ab + NA - 1;
+                B6D_STEP(0, 1, 0, 1, s, ab, an0);
+            }
+        } else {
+            // three X register sets (set of step k: k % 3) and two B buffers: six steps per
+            // iteration, the rest peeled one by one (NA 2: ring slot k % 2 = B buffer parity)
+            for (; s + 5 < S; s += 6) {
+                B6D_STEP(0, 1, 0, 1, s, 0, 1);
+                B6D_STEP(1, 0, 1, 2, s + 1, 1, 0);
+                B6D_STEP(0, 1, 2, 0, s + 2, 0, 1);
+                B6D_STEP(1, 0, 0, 1, s + 3, 1, 0);
+                B6D_STEP(0, 1, 1, 2, s + 4, 0, 1);
+                B6D_STEP(1, 0, 2, 0, s + 5, 1, 0);
+            }
+            if (s < S) B6D_STEP(0, 1, 0, 1, s, 0, 1);
+            if (s + 1 < S) B6D_STEP(1, 0, 1, 2, s + 1, 1, 0);
+            if (s + 2 < S) B6D_STEP(0, 1, 2, 0, s + 2, 0, 1);
+            if (s + 3 < S) B6D_STEP(1, 0, 0, 1, s + 3, 1, 0);
+            if (s + 4 < S) B6D_STEP(0, 1, 1, 2, s + 4, 0, 1);
         }
 #undef B6D_STEP
 #undef B6D_BARRIER
@@ -4664,25 +4688,28 @@ int niidmix_mix_dense_bf16x6_f32(const float *x, int64_t ld_x, float *y, int64_t
         hipLaunchKernelGGL((k_mix_dense_b6<WN, SC, AB, TM>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                            x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
     } while (0)
-    // W tiles by LDS-DMA (k_mix_dense_b6d): NIIDMIX_DENSE_B6_DMA = "WN,NA" -- 4,3 (256 x 256, one
-    // block per CU, W two K-steps ahead), 4,2, or 2,2 (256 x 128, two blocks per CU)
+    // W tiles by LDS-DMA (k_mix_dense_b6d): NIIDMIX_DENSE_B6_DMA = "WN,NA[,XD]" -- 4,3 (256 x 256,
+    // one block per CU, W two K-steps ahead), 4,2, or 2,2 (256 x 128, two blocks per CU); XD 3:
+    // X fetched three K-steps ahead (a third register set, with the 2-deep W ring)
     if (const char *e = getenv("NIIDMIX_DENSE_B6_DMA")) {
-        int dwn = 0, dna = 0;
-        if (sscanf(e, "%d,%d", &dwn, &dna) == 2 && dwn != 0) {
-#define NIIDMIX_B6D(WN, NA) do { \
+        int dwn = 0, dna = 0, dxd = 2;
+        if (sscanf(e, "%d,%d,%d", &dwn, &dna, &dxd) >= 2 && dwn != 0) {
+#define NIIDMIX_B6D(WN, NA, XD) do { \
             const int64_t n_it = mpad / 256, n_jt = (p + 64 * WN - 1) / (64 * WN); \
             const int64_t n_items = n_it * ((n_jt + 7) / 8) * 8; \
             const size_t lds = ((size_t)NA * 3 * 256 * 2 + (size_t)2 * 3 * 64 * WN * 2) * sizeof(uint4); \
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6d<WN, 4, NA>), \
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mix_dense_b6d<WN, 4, NA, XD>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
                 return set_error(NIIDMIX_EHIP, "k_mix_dense_b6d: %zu B of LDS refused", lds); \
-            hipLaunchKernelGGL((k_mix_dense_b6d<WN, 4, NA>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
+            hipLaunchKernelGGL((k_mix_dense_b6d<WN, 4, NA, XD>), dim3((unsigned)grid_for(n_items)), dim3(128 * WN), lds, s, \
                                x, ld_x, y, ld_y, n, p, wp, mpad, kpad, n_it, n_items, row_ptr, col, val); \
         } while (0)
-            if (dwn == 4 && dna == 3) NIIDMIX_B6D(4, 3);
-            else if (dwn == 4 && dna == 2) NIIDMIX_B6D(4, 2);
-            else if (dwn == 2 && dna == 2) NIIDMIX_B6D(2, 2);
-            else return set_error(NIIDMIX_EINVAL, "NIIDMIX_DENSE_B6_DMA=%s: 4,3 / 4,2 / 2,2", e);
+            if (dwn == 4 && dna == 3 && dxd == 2) NIIDMIX_B6D(4, 3, 2);
+            else if (dwn == 4 && dna == 2 && dxd == 2) NIIDMIX_B6D(4, 2, 2);
+            else if (dwn == 4 && dna == 2 && dxd == 3) NIIDMIX_B6D(4, 2, 3);
+            else if (dwn == 2 && dna == 2 && dxd == 2) NIIDMIX_B6D(2, 2, 2);
+            else if (dwn == 2 && dna == 2 && dxd == 3) NIIDMIX_B6D(2, 2, 3);
+            else return set_error(NIIDMIX_EINVAL, "NIIDMIX_DENSE_B6_DMA=%s: 4,3 / 4,2[,3] / 2,2[,3]", e);
 #undef NIIDMIX_B6D
             return check_launch("k_mix_dense_b6d");
         }

@@ -44,8 +44,24 @@ def build(force=False, verbose=True):
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    _check_undefined(LIB + ".tmp")
     os.replace(LIB + ".tmp", LIB)
     return LIB
+
+
+def _check_undefined(path):
+    """Fail the build when a kernel's host stub is missing: hipcc can leave a template kernel's
+    launch stub undefined (a construct the host pass rejects without a diagnostic), and the
+    library then only fails at dlopen on the GPU box."""
+    nm = shutil.which("nm")
+    if nm is None:
+        return
+    out = subprocess.run([nm, "-D", "--undefined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "_GLOBAL__N_" in ln]
+    if bad:
+        os.remove(path)
+        raise RuntimeError("libniidmix: undefined kernel symbols: " + ", ".join(bad[:4]))
 
 
 if __name__ == "__main__":

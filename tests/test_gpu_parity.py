@@ -837,14 +837,15 @@ def test_dense_b6_tail_rows_not_read(gpu):
 
 
 @pytest.mark.parametrize("variant", [("NIIDMIX_DENSE_B6_W1", "1"), ("NIIDMIX_DENSE_B6_DMA", "4,3"),
-                                     ("NIIDMIX_DENSE_B6_DMA", "4,2"), ("NIIDMIX_DENSE_B6_DMA", "2,2")])
+                                     ("NIIDMIX_DENSE_B6_DMA", "4,2"), ("NIIDMIX_DENSE_B6_DMA", "2,2"),
+                                     ("NIIDMIX_DENSE_B6_DMA", "4,2,3"), ("NIIDMIX_DENSE_B6_DMA", "2,2,3")])
 @pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (257, 1030), (300, 70000)])
 def test_dense_b6_variants_bitwise(n, p, variant, gpu, monkeypatch):
     """The bf16x6 kernel's variants run the same products in the same K order through the same
     MFMA per output element as the default (8 waves of 128 x 64, W through registers), so their
     outputs are bit-identical, non-finite guard included: one wave per SIMD (k_mix_dense_b6w, 4
     waves of 128 x 128) and the W tiles by LDS-DMA (k_mix_dense_b6d, round 6: 256 x 256 with a
-    three- or two-deep W ring, and 256 x 128 blocks two per CU)."""
+    three- or two-deep W ring, and 256 x 128 blocks two per CU; X three K-steps ahead)."""
     ops = _ops()
     rng = np.random.default_rng(7 * n + p)
     w = rng.random((n, n)).astype(np.float32) + np.float32(0.01)

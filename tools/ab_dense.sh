@@ -5,9 +5,9 @@ set -u
 O=${1:?out dir}; REPS=${REPS:-2}
 mkdir -p "$O"
 for rep in $(seq 1 $REPS); do
-  for v in default 4,3 4,2 2,2; do
+  for v in ${VARIANTS:-default 4,3 4,2 2,2}; do
     if [ $v = default ]; then unset NIIDMIX_DENSE_B6_DMA; else export NIIDMIX_DENSE_B6_DMA=$v; fi
-    f=$O/bench_${v/,/_}_$rep.json
+    f=$O/bench_${v//,/_}_$rep.json
     timeout -k 10 120 python bench.py --no-cpu-baseline --config fc1000 --kernel dense --steps 10 --warmup 3 > $f 2> $f.err || { echo "bench $v failed"; tail -5 $f.err; exit 4; }
     python -c "import json;d=json.load(open('$f'));print('$v', d['ms_per_step'], d['roofline']['frac'])"
   done
