@@ -902,7 +902,12 @@ __device__ __forceinline__ const float *qrow(const float *base, int row, int64_t
         return base + (int64_t)row * ld + lo;
 }
 
-template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32>
+// MS (member split, round 6; NIIDMIX_CLIQUE_QM): MS lane quarters share one clique, quarter q taking
+// members q % MS, q % MS + MS, ... of each wave's slots; the group sums add those quarters' partials
+// after the cross-wave reduction.  MS = Q: an item is one clique x 64 columns, so a chunk's 100
+// items (10 000 nodes) rather than 25 are spread over the XCD's blocks in flight: fewer chunks in
+// flight per XCD, whose rows the gateway gathers then find in its L2.  MS = 1: Q cliques per item.
+template <int WAVES, int RPW, int G, int Q, int OCC, int GA, bool OFF32, int MS = 1>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_mix_clique_q(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
@@ -945,10 +950,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     bool d_multi = false;
     if (lane < Q * RPW) {
         const int dq = lane / RPW, dr = lane - (lane / RPW) * RPW;
-        const int64_t c = cg * Q + dq;
+        const int64_t c = cg * (Q / MS) + dq / MS;
         if (c < n_cliques) {
             const int32_t m0 = clique_ptr[c], M = clique_ptr[c + 1] - m0;
-            const int k = wave + WAVES * dr;
+            const int k = dq % MS + MS * (wave + WAVES * dr);
             if (k < M) {
                 const int32_t m = m0 + k;
                 d_rg = member_row[m] | ((member_group[m] & kMemberGroupMask) << 28);
@@ -1031,12 +1036,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     }
     // members with several residual entries (rare): the rest one by one, per lane
     if (multi) {
-        const int64_t c = cg * Q + q;
+        const int64_t c = cg * (Q / MS) + q / MS;
         const int32_t m0 = c < n_cliques ? clique_ptr[c] : 0;
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
             if (__shfl(d_rg, sl0 + r) < 0) continue;
-            const int32_t m = m0 + wave + WAVES * r;
+            const int32_t m = m0 + q % MS + MS * (wave + WAVES * r);
             const int rb = res_ptr[m], re = res_ptr[m + 1];
             for (int j = rb + 1; j < re; ++j) {
                 const float w = res_val[j];
@@ -1062,7 +1067,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(OCC,
     float sg[G][4];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const float4 a = tot[g][lane];
+        const int q0 = q - q % MS;             // the clique's first quarter
+        float4 a = tot[g][q0 * LQ + lc];
+#pragma unroll
+        for (int qq = 1; qq < MS; ++qq) {      // the clique's group sums: its quarters' partials
+            const float4 b = tot[g][(q0 + qq) * LQ + lc];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
         sg[g][0] = a.x; sg[g][1] = a.y; sg[g][2] = a.z; sg[g][3] = a.w;
     }
     uint32_t bad = 0;                          // this lane's slots with a non-finite output
@@ -3875,13 +3886,13 @@ int launch_clique_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
 // of <= 112 members).  Chosen when a 256-column chunk of all member rows (n_members KB) would not
 // fit an XCD's L2; NIIDMIX_CLIQUE_Q=1 disables it, =4 forces it (A/B).
 constexpr int64_t kQRowsMin = 4096;
-template <int G, int W, int R, int OCC, int GA, int Q>
+template <int G, int W, int R, int OCC, int GA, int Q, int MS = 1>
 int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                     const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
     constexpr int64_t CW = 4 * (64 / Q);
     constexpr int CW_SHIFT = Q == 8 ? 5 : 6;
     if (bg.bc_shift < CW_SHIFT) return set_error(NIIDMIX_EINVAL, "%d-column items do not fit %d-column blocks", (int)CW, 1 << bg.bc_shift);
-    const int64_t n_cg = (pl->n_cliques + Q - 1) / Q;
+    const int64_t n_cg = (pl->n_cliques + Q / MS - 1) / (Q / MS);
     const int64_t n_chunks = (p + CW - 1) / CW;
     const int64_t n_items = n_cg * ((n_chunks + 7) / 8) * 8;
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (clique group, chunk) items for one grid");
@@ -3898,20 +3909,20 @@ int launch_clique_q(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_
         if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
         if (k > 0 && (int64_t)k * n_cu < n_items) grid = (int64_t)k * n_cu / 8 * 8;
     }
-#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O>), dim3((unsigned)grid), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
+#define NIIDMIX_CQ(O) hipLaunchKernelGGL((k_mix_clique_q<W, R, G, Q, OCC, GA, O, MS>), dim3((unsigned)grid), dim3(W * 64), 0, s, x, ld_x, y, ld_y, p, pl->n_cliques, pl->clique_ptr, pl->member_row, pl->member_group, pl->coef, pl->res_ptr, pl->res_col, pl->res_val, n_cg, n_items, cpb, bg.bs_x, bg.bs_y, pl->csr_ptr, pl->csr_col, pl->csr_val)
     if (off32) NIIDMIX_CQ(true); else NIIDMIX_CQ(false);
 #undef NIIDMIX_CQ
     return check_launch("k_mix_clique_q");
 }
 
-template <int W, int R, int OCC, int GA, int Q = 4>
+template <int W, int R, int OCC, int GA, int Q = 4, int MS = 1>
 int launch_clique_q_g(const float *x, int64_t ld_x, float *y, int64_t ld_y, int64_t p,
                       const niidmix_clique_plan *pl, hipStream_t s, const BlockGeom &bg) {
     switch (pl->n_groups) {
-        case 1: return launch_clique_q<1, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 2: return launch_clique_q<2, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 3: return launch_clique_q<3, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
-        case 4: return launch_clique_q<4, W, R, OCC, GA, Q>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 1: return launch_clique_q<1, W, R, OCC, GA, Q, MS>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 2: return launch_clique_q<2, W, R, OCC, GA, Q, MS>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 3: return launch_clique_q<3, W, R, OCC, GA, Q, MS>(x, ld_x, y, ld_y, p, pl, s, bg);
+        case 4: return launch_clique_q<4, W, R, OCC, GA, Q, MS>(x, ld_x, y, ld_y, p, pl, s, bg);
         default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", pl->n_groups);
     }
 }
@@ -3947,6 +3958,18 @@ int launch_clique_tiled(const float *x, int64_t ld_x, float *y, int64_t ld_y, in
         if (qw == 0) {
             if (mc <= 104) { qw = 8; qr = 13; qo = 4; qg = 13; }
             else { qw = 16; qr = 7; qo = 8; qg = 2; }
+        }
+        // NIIDMIX_CLIQUE_QM=W,R,OCC[,MS]: the member-split tile (MS lane quarters per clique,
+        // default 4: one clique per item; W waves x MS quarters x R slots >= the clique)
+        if (const char *e = getenv("NIIDMIX_CLIQUE_QM")) {
+            int mw = 0, mr = 0, mo = 0, ms = 4;
+            if (sscanf(e, "%d,%d,%d,%d", &mw, &mr, &mo, &ms) >= 3 && mw > 0) {
+                if (mw * mr * ms < mc) return set_error(NIIDMIX_EINVAL, "member-split tile %dx%dx%d < %d members", mw, ms, mr, mc);
+#define NIIDMIX_QM(W, R, O, M) if (mw == W && mr == R && mo == O && ms == M) return launch_clique_q_g<W, R, O, R, 4, M>(x, ld_x, y, ld_y, p, pl, s, bg)
+                NIIDMIX_QM(8, 4, 4, 4); NIIDMIX_QM(16, 2, 8, 4); NIIDMIX_QM(8, 7, 4, 2); NIIDMIX_QM(16, 4, 4, 2);
+#undef NIIDMIX_QM
+                return set_error(NIIDMIX_EUNSUPPORTED, "no member-split tile %s", e);
+            }
         }
         if (qw * qr < mc) return set_error(NIIDMIX_EINVAL, "clique tile %dx%d < %d members", qw, qr, mc);
 #define NIIDMIX_QT(W, R, O, GA, QQ) if (qw == W && qr == R && qo == O && qg == GA && qq == QQ) return launch_clique_q_g<W, R, O, GA, QQ>(x, ld_x, y, ld_y, p, pl, s, bg)

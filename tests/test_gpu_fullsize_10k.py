@@ -59,11 +59,14 @@ def _blocked_colsum_gap(xb, yb):
     return gap
 
 
-@pytest.mark.parametrize("bc_env", ["", "256"])
-def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod, monkeypatch, bc_env):
+@pytest.mark.parametrize("bc_env,qm", [("", ""), ("256", ""), ("", "8,4,4"), ("", "8,7,4,2"), ("", "16,4,4,2")])
+def test_dcliques10000_single_gpu_as_benched(dc10k, gpu, oracle_mod, monkeypatch, bc_env, qm):
+    """qm: the member-split multi-clique tile (NIIDMIX_CLIQUE_QM=W,R,OCC, round 6)."""
     from niidmix import memory, ops
     if bc_env:
         monkeypatch.setenv("NIIDMIX_Q_BLOCK_COLS", bc_env)
+    if qm:
+        monkeypatch.setenv("NIIDMIX_CLIQUE_QM", qm)
     csr, cliques = dc10k
     m = ops.Mixer(csr=csr, cliques=cliques, device=gpu)
     assert m.kernel_for("fast") == "clique" and m.plan.max_clique_res == 99

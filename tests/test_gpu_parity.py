@@ -594,6 +594,36 @@ def test_multi_clique_tile_vs_golden(name, tile, gpu, oracle_mod, monkeypatch):
         assert oracle_mod.bitwise_equal(memory.from_blocked(yb, p).cpu().numpy(), y), (name, tile, bc)
 
 
+@pytest.mark.parametrize("qm", ["8,4,4", "8,7,4,2", "16,4,4,2"])
+@pytest.mark.parametrize("name", golden_cases())
+def test_member_split_tile_vs_golden(name, qm, gpu, oracle_mod, monkeypatch):
+    """The member-split multi-clique tile (round 6, NIIDMIX_CLIQUE_QM: one clique per item, the
+    lane quarters split its members) forced on every golden clique case, non-finite fixtures
+    included: row-major and column-blocked slabs within the tolerance with the reference's inf /
+    NaN pattern, blocked == row-major bitwise."""
+    from niidmix import memory
+    g = load_golden(name)
+    m = _mixer(g, gpu)
+    p = g["x"].shape[1]
+    if m.plan is None or p % 4:
+        pytest.skip("no clique plan / p % 4")
+    f = [int(v) for v in qm.split(",")]
+    w, r, ms = f[0], f[1], (f[3] if len(f) > 3 else 4)
+    if m.plan.max_clique > 112 or ms * w * r < m.plan.max_clique:
+        pytest.skip("clique larger than the tile")
+    monkeypatch.setenv("NIIDMIX_CLIQUE_Q", "4")
+    monkeypatch.setenv("NIIDMIX_CLIQUE_QM", qm)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="clique").cpu().numpy()
+    bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+    ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+    assert ok, (name, qm, worst)
+    for bc in (64, 256):
+        yb = memory.empty_blocked(m.n, p, gpu, bc)
+        m.mix_blocked(memory.to_blocked(x, bc), yb, p)
+        assert oracle_mod.bitwise_equal(memory.from_blocked(yb, p).cpu().numpy(), y), (name, qm, bc)
+
+
 @pytest.mark.parametrize("n,inter,size", [(4000, "fully-connected", 100), (5000, "smallworld", 100),
                                           (4200, "ring", 100), (4400, "smallworld", 110),
                                           (4480, "fully-connected", 112)])
