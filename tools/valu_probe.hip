@@ -17,6 +17,7 @@ __global__ __launch_bounds__(256) void k(float *out, float w, int sel, long long
     float nz = -0.0f * w;
     const int idxv = (int)(threadIdx.x * 7 + sel) & 1023;
     const long long c0 = clock64(), r0w = wall_clock64();
+#pragma unroll 2
     for (int it = 0; it < ITERS; ++it) {
         asm volatile("" : "+v"(tp));
         if (KIND == 0) {            // 16 v_pk_add_f32
@@ -73,6 +74,14 @@ __global__ __launch_bounds__(256) void k(float *out, float w, int sel, long long
             } else {
                 acc = acc + T;
             }
+        } else if (KIND == 14) {  // 16 pk_add, accumulator pairs in banks 0-1, shared operand in 2-3
+            asm volatile("v_mov_b64 v[66:67], %0\nv_pk_add_f32 v[0:1], v[0:1], v[66:67]\nv_pk_add_f32 v[4:5], v[4:5], v[66:67]\nv_pk_add_f32 v[8:9], v[8:9], v[66:67]\nv_pk_add_f32 v[12:13], v[12:13], v[66:67]\nv_pk_add_f32 v[16:17], v[16:17], v[66:67]\nv_pk_add_f32 v[20:21], v[20:21], v[66:67]\nv_pk_add_f32 v[24:25], v[24:25], v[66:67]\nv_pk_add_f32 v[28:29], v[28:29], v[66:67]\nv_pk_add_f32 v[32:33], v[32:33], v[66:67]\nv_pk_add_f32 v[36:37], v[36:37], v[66:67]\nv_pk_add_f32 v[40:41], v[40:41], v[66:67]\nv_pk_add_f32 v[44:45], v[44:45], v[66:67]\nv_pk_add_f32 v[48:49], v[48:49], v[66:67]\nv_pk_add_f32 v[52:53], v[52:53], v[66:67]\nv_pk_add_f32 v[56:57], v[56:57], v[66:67]\nv_pk_add_f32 v[60:61], v[60:61], v[66:67]" :: "v"(tp) : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67");
+        } else if (KIND == 15) {  // 16 pk_add, accumulator pairs and shared operand all in banks 2-3
+            asm volatile("v_mov_b64 v[66:67], %0\nv_pk_add_f32 v[2:3], v[2:3], v[66:67]\nv_pk_add_f32 v[6:7], v[6:7], v[66:67]\nv_pk_add_f32 v[10:11], v[10:11], v[66:67]\nv_pk_add_f32 v[14:15], v[14:15], v[66:67]\nv_pk_add_f32 v[18:19], v[18:19], v[66:67]\nv_pk_add_f32 v[22:23], v[22:23], v[66:67]\nv_pk_add_f32 v[26:27], v[26:27], v[66:67]\nv_pk_add_f32 v[30:31], v[30:31], v[66:67]\nv_pk_add_f32 v[34:35], v[34:35], v[66:67]\nv_pk_add_f32 v[38:39], v[38:39], v[66:67]\nv_pk_add_f32 v[42:43], v[42:43], v[66:67]\nv_pk_add_f32 v[46:47], v[46:47], v[66:67]\nv_pk_add_f32 v[50:51], v[50:51], v[66:67]\nv_pk_add_f32 v[54:55], v[54:55], v[66:67]\nv_pk_add_f32 v[58:59], v[58:59], v[66:67]\nv_pk_add_f32 v[62:63], v[62:63], v[66:67]" :: "v"(tp) : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67");
+        } else if (KIND == 16) {  // 16 pk_add, accumulator pairs consecutive (v[0:1], v[2:3], ...)
+            asm volatile("v_mov_b64 v[66:67], %0\nv_pk_add_f32 v[0:1], v[0:1], v[66:67]\nv_pk_add_f32 v[2:3], v[2:3], v[66:67]\nv_pk_add_f32 v[4:5], v[4:5], v[66:67]\nv_pk_add_f32 v[6:7], v[6:7], v[66:67]\nv_pk_add_f32 v[8:9], v[8:9], v[66:67]\nv_pk_add_f32 v[10:11], v[10:11], v[66:67]\nv_pk_add_f32 v[12:13], v[12:13], v[66:67]\nv_pk_add_f32 v[14:15], v[14:15], v[66:67]\nv_pk_add_f32 v[16:17], v[16:17], v[66:67]\nv_pk_add_f32 v[18:19], v[18:19], v[66:67]\nv_pk_add_f32 v[20:21], v[20:21], v[66:67]\nv_pk_add_f32 v[22:23], v[22:23], v[66:67]\nv_pk_add_f32 v[24:25], v[24:25], v[66:67]\nv_pk_add_f32 v[26:27], v[26:27], v[66:67]\nv_pk_add_f32 v[28:29], v[28:29], v[66:67]\nv_pk_add_f32 v[30:31], v[30:31], v[66:67]" :: "v"(tp) : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67");
+        } else if (KIND == 17) {  // kind 14 without the compiler's unroll (a branch per 17 instructions)
+            asm volatile("v_mov_b64 v[66:67], %0\nv_pk_add_f32 v[0:1], v[0:1], v[66:67]\nv_pk_add_f32 v[2:3], v[2:3], v[66:67]\nv_pk_add_f32 v[4:5], v[4:5], v[66:67]\nv_pk_add_f32 v[6:7], v[6:7], v[66:67]\nv_pk_add_f32 v[8:9], v[8:9], v[66:67]\nv_pk_add_f32 v[10:11], v[10:11], v[66:67]\nv_pk_add_f32 v[12:13], v[12:13], v[66:67]\nv_pk_add_f32 v[14:15], v[14:15], v[66:67]\nv_pk_add_f32 v[16:17], v[16:17], v[66:67]\nv_pk_add_f32 v[18:19], v[18:19], v[66:67]\nv_pk_add_f32 v[20:21], v[20:21], v[66:67]\nv_pk_add_f32 v[22:23], v[22:23], v[66:67]\nv_pk_add_f32 v[24:25], v[24:25], v[66:67]\nv_pk_add_f32 v[26:27], v[26:27], v[66:67]\nv_pk_add_f32 v[28:29], v[28:29], v[66:67]\nv_pk_add_f32 v[30:31], v[30:31], v[66:67]" :: "v"(tp) : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67");
         } else if (KIND == 8) {     // select by bit-field insert, SALU row mask: 16 s_bfe + 32 v_bfi + 16 pk_add
             const int m = __builtin_amdgcn_readfirstlane(sel + it);
 #pragma unroll
@@ -116,8 +125,10 @@ static const char *names[] = {"16 pk_add (compiler)", "32 v_add_f32", "16 pk_add
                               "16 pk_add + gpr_idx save/restore", "32 v_mov", "16 pk_mul (asm)", "16 pk_fma (asm)",
                               "bfi select, SALU mask: 32 v_bfi + 16 pk_add", "bfi select, VALU mask: 16 v_bfe + 32 v_bfi + 16 pk_add",
                               "16 pk_add + gpr_idx, index by v_readlane", "16 pk_add + v_readlane->s_cmp->branch",
-                              "16 pk_add, SGPR-bit branch, 1/8 save/restore", "16 pk_add, SGPR-bit branch never taken"};
-static const int instrs[] = {16, 32, 16, 48, 16, 32, 16, 16, 48, 64, 16, 16, 16, 16};
+                              "16 pk_add, SGPR-bit branch, 1/8 save/restore", "16 pk_add, SGPR-bit branch never taken",
+                              "16 pk_add, no VGPR bank conflict (+1 v_mov_b64)", "16 pk_add, every one bank-conflicted (+1 mov)",
+                              "16 pk_add, consecutive pairs (+1 mov)", "16 pk_add, consecutive pairs, loop not unrolled"};
+static const int instrs[] = {16, 32, 16, 48, 16, 32, 16, 16, 48, 64, 16, 16, 16, 16, 17, 17, 17, 17};
 
 template <int KIND>
 void run(float *out, long long *tick, int blocks_per_cu) {
@@ -157,6 +168,7 @@ int main() {
     // back-to-back packed and scalar fp32 adds at one and two waves per SIMD
     for (int occ : {1, 2, 4}) {
         run<2>(out, tick, occ); run<1>(out, tick, occ); run<0>(out, tick, occ); run<7>(out, tick, occ);
+        run<14>(out, tick, occ); run<15>(out, tick, occ); run<16>(out, tick, occ);
     }
     for (int occ : {2, 4}) { run<4>(out, tick, occ); run<3>(out, tick, occ); }
     hipFree(out);
