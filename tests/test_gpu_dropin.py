@@ -368,6 +368,48 @@ def test_read_guard_unpredicted_reader(gpu, oracle_mod, monkeypatch):
     assert any(not torch.equal(u, v) for u, v in zip(stale, ref))
 
 
+@pytest.mark.parametrize("stripes", [1, 3])
+def test_resident_device_step_resident_params(stripes, gpu, oracle_mod):
+    """niidmix.slab.ResidentRound with the plain device step (fused_op without gradient averaging)
+    over 1 and 3 column stripes of one GPU: round 0 sends parameters and gradients, rounds 1-3 only
+    gradients (begin(resident_in0=True): the last round's output buffer becomes the input); every
+    round bitwise torch's CPU SGD step (p.add_(g, alpha=-lr)) followed by the C oracle's mixing,
+    with -0.0 gradients and parameters planted."""
+    from niidmix import ops
+    from niidmix.slab import ResidentRound, fused_op
+    from niidmix.topology import mh_csr
+    n, p, lr = 12, 3000, 0.05
+    edges = {r: [(r + 1) % n, (r - 1) % n, (r + 5) % n] for r in range(n)}
+    csr = mh_csr(n, {r: sorted(set(e)) for r, e in edges.items()})
+    mixer = ops.Mixer(csr=csr, device=gpu)
+    gen = torch.Generator().manual_seed(stripes)
+    host_p = torch.randn(n, p, generator=gen).pin_memory()
+    host_p[::4, ::5] = -0.0
+    host_g = torch.empty(n, p).pin_memory()
+    rr = ResidentRound(lambda dev, part: fused_op(dev, part, None, list(range(n)), lr, mixer),
+                       n, p, [gpu] * stripes, block=4, align=256, n_in=2, n_out=1)
+    assert len(rr.parts) == stripes
+    ref = host_p.clone()
+    for k in range(4):
+        g = torch.randn(n, p, generator=gen)
+        g[::3, ::7] = -0.0
+        g[1::3, ::11] = 0.0
+        host_g.copy_(g)
+        if k == 0:
+            rr.begin(host_p, host_g, outs=(host_p,))
+        else:
+            assert rr.current()
+            rr.begin(None, host_g, outs=(host_p,), resident_in0=True)
+        for i in range(n):
+            rr.row_ready(i)
+        rr.mix("exact")
+        rr.wait_all()
+        with torch.no_grad():
+            ref.add_(g, alpha=-lr)
+        ref = torch.from_numpy(oracle_mod.mix_exact_c(ref.numpy(), csr.row_ptr, csr.col, csr.val))
+        assert oracle_mod.bitwise_equal(host_p.numpy(), ref.numpy()), k
+
+
 @pytest.mark.parametrize("step", ["device", "cpu"])
 def test_training_rounds_device_step(step, gpu, oracle_mod, monkeypatch):
     """the plain round with its optimizer step on the device (_FusedEngine(plain):

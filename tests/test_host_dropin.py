@@ -324,3 +324,39 @@ def test_logger_install_hooks_cpu(monkeypatch, tmp_path):
     assert done == ["simulate.logger.Logger.log_consensus_distance", "setup.model.average"]
     assert sm.average is nl.average
     assert nl.install_hooks({"logger": {"log-global-model-accuracy": True}}) == done
+
+
+def test_device_step_eligibility(monkeypatch):
+    """niidmix.d_sgd._device_step_ok: the plain round's optimizer step moves to the device only for
+    the plugin's plain SGD (momentum, dampening, weight decay 0, no Nesterov / maximize) at
+    params' learning rate over exactly the model's parameters; NIIDMIX_DEVICE_STEP=0 and
+    NIIDMIX_RESIDENT=0 turn it off (no GPU needed)."""
+    from niidmix import d_sgd
+    monkeypatch.delenv("NIIDMIX_DEVICE_STEP", raising=False)
+    monkeypatch.delenv("NIIDMIX_RESIDENT", raising=False)
+    params = {"algorithm": {"learning-rate": 0.1, "learning-momentum": 0.0}}
+
+    def nodes_with(**kw):
+        out = []
+        for r in range(3):
+            m = torch.nn.Linear(4, 2)
+            opt = d_sgd.optimizer(m, params) if not kw else torch.optim.SGD(m.parameters(), **kw)
+            out.append({"rank": r, "model": m, "optimizer": opt})
+        return out
+
+    assert d_sgd._device_step_ok(params, nodes_with())
+    assert not d_sgd._device_step_ok(params, nodes_with(lr=0.1, momentum=0.9))
+    assert not d_sgd._device_step_ok(params, nodes_with(lr=0.1, weight_decay=1e-4))
+    assert not d_sgd._device_step_ok(params, nodes_with(lr=0.2))
+    assert not d_sgd._device_step_ok(params, nodes_with(lr=0.1, momentum=0.9, nesterov=True))
+    nd = nodes_with()
+    nd[1]["optimizer"] = torch.optim.SGD([next(nd[1]["model"].parameters())], lr=0.1)
+    assert not d_sgd._device_step_ok(params, nd)          # not every parameter
+    nd = nodes_with()
+    nd[2]["optimizer"] = torch.optim.Adam(nd[2]["model"].parameters(), lr=0.1)
+    assert not d_sgd._device_step_ok(params, nd)
+    monkeypatch.setenv("NIIDMIX_DEVICE_STEP", "0")
+    assert not d_sgd._device_step_ok(params, nodes_with())
+    monkeypatch.delenv("NIIDMIX_DEVICE_STEP")
+    monkeypatch.setenv("NIIDMIX_RESIDENT", "0")
+    assert not d_sgd._device_step_ok(params, nodes_with())
