@@ -719,6 +719,45 @@ def test_randomize_keeps_slab(gpu, oracle_mod):
         topo = d_sgd.randomized_topology(nodes, params, None)
 
 
+def test_randomize_training_rounds_device_step(gpu, oracle_mod):
+    """--randomize through next_step with the device step (the plain round's default): a new graph
+    every round (d_sgd.py:223-234) swaps only the mixing operator of the resident engine
+    (_FusedEngine.set_topology): the same engine, slab and resident parameters every round (one
+    parameter upload), and every round bitwise the reference loop (CPU SGD + the reference mixing
+    on that round's graph)."""
+    from niidmix import d_sgd
+    n = 24
+
+    def run(mix):
+        params, nodes, _ = _ring_training_setup(n, seed=5)
+        params["topology"] = {"name": "random-graph", "nb-neighbours": 4, "topology-seed": 3,
+                              "weights": "metropolis-hasting", "randomize": True}
+        topo = d_sgd.randomized_topology(nodes, params, None)
+        orig, orig_rs = d_sgd.average, d_sgd._row_streamed
+        if mix == "oracle":
+            d_sgd.average = lambda nds, t, p: oracle_mod.reference_loop_average(nds, t)
+            d_sgd._row_streamed = lambda p: False
+        snaps, engs = [], []
+        try:
+            state, _, _ = d_sgd.init(nodes, topo, params)
+            for _ in range(5):
+                state, _, _, _ = d_sgd.next_step(state, params, None)
+                engs.append(d_sgd.round_engine(nodes))
+                d_sgd.synchronize()
+                snaps.append(torch.stack([torch.cat([q.detach().reshape(-1)
+                                                     for q in nd["model"].parameters()])
+                                          for nd in nodes]).clone())
+        finally:
+            d_sgd.average, d_sgd._row_streamed = orig, orig_rs
+        return snaps, engs
+
+    a, engs = run("gpu")
+    b, _ = run("oracle")
+    for k, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u.view(torch.int32), v.view(torch.int32)), k
+    assert all(e is engs[0] for e in engs) and engs[0].plain and engs[0].param_uploads == 1
+
+
 @pytest.mark.parametrize("mode", ["exact", "fast"])
 def test_sparse_topology_plugin_round(mode, gpu, oracle_mod, tmp_path, monkeypatch):
     """Sparse ingestion under the unchanged run.py: a rundir written by niidmix.sparse_topology,
