@@ -26,6 +26,7 @@ import json
 import logging
 import os
 import time
+import weakref
 from random import Random
 
 import torch
@@ -180,9 +181,12 @@ def gradient(nodes, topology, params):
         nodes[r]["optimizer"].step()
 
 
-_sgd_checked = {}
-# node lists whose device-step buffers did not fit in HBM (the CPU steps them)
-_no_device_step = set()
+# optimizer -> weakref of the model whose parameters it was checked to cover (no strong refs: a
+# dropped node list is not kept alive here)
+_sgd_checked = weakref.WeakKeyDictionary()
+# node lists whose device-step buffers did not fit in HBM (the CPU steps them): id -> weakref of
+# the list's first model (an id reused by another list is not taken for it)
+_no_device_step = {}
 
 
 def _device_step_ok(params, nodes):
@@ -190,8 +194,10 @@ def _device_step_ok(params, nodes):
     node's optimizer is the plugin's plain SGD (optimizer() above, momentum 0: no state, p += -lr g)
     over exactly its model's parameters, at params' learning rate; NIIDMIX_DEVICE_STEP=0 disables
     it (the CPU steps, as rounds 1-5 did)."""
-    if os.environ.get("NIIDMIX_DEVICE_STEP", "1") == "0" or not _resident_ok() or \
-            id(nodes) in _no_device_step:
+    if os.environ.get("NIIDMIX_DEVICE_STEP", "1") == "0" or not _resident_ok():
+        return False
+    hit = _no_device_step.get(id(nodes))
+    if hit is not None and nodes and hit() is nodes[0]["model"]:
         return False
     lr = float(params["algorithm"]["learning-rate"])
     for nd in nodes:
@@ -202,13 +208,13 @@ def _device_step_ok(params, nodes):
         if (float(g["lr"]) != lr or g["momentum"] != 0 or g["dampening"] != 0 or
                 g["weight_decay"] != 0 or g["nesterov"] or g.get("maximize", False)):
             return False
-        hit = _sgd_checked.get(id(opt))
-        if hit is None or hit[0] is not opt or hit[1] is not nd["model"]:
+        hit = _sgd_checked.get(opt)
+        if hit is None or hit() is not nd["model"]:
             with guard.suspended():
                 mine = list(nd["model"].parameters())
             if len(g["params"]) != len(mine) or any(a is not b for a, b in zip(g["params"], mine)):
                 return False
-            _sgd_checked[id(opt)] = (opt, nd["model"])
+            _sgd_checked[opt] = weakref.ref(nd["model"])
     return True
 
 
@@ -498,7 +504,8 @@ class _Engine:
 
 
 _engines = {}
-# the engine that ran the last row-streamed next_step round of a node list (round_engine)
+# the engine that ran the last row-streamed next_step round of a node list (round_engine), held
+# weakly: an engine evicted from the caches frees its HBM buffers
 _last_round = {}
 # engines (pinned slab + device buffers) kept per node list, the most recent ones
 MAX_ENGINES = int(os.environ.get("NIIDMIX_MAX_ENGINES", 4))
@@ -524,7 +531,8 @@ def invalidate(nodes=None):
 def round_engine(nodes):
     """The engine (_Engine or _FusedEngine, with .resident) whose row-streamed round last ran for
     this node list in next_step, or None."""
-    return _last_round.get(id(nodes))
+    ref = _last_round.get(id(nodes))
+    return ref() if ref is not None else None
 
 
 def synchronize():
@@ -731,7 +739,7 @@ def next_step(state, params, rundir):
         feng = _fused_engine(active, topology, params, plain=True)
         if feng.resident is None:                 # the buffers do not fit: CPU step, windowed
             _fused_engines.pop((id(active), True), None)
-            _no_device_step.add(id(active))
+            _no_device_step[id(active)] = weakref.ref(active[0]["model"])
             feng = None
     eng = _engine(active, topology) if streamed and feng is None else None
     # gradient averaging, momentum 0: the fused device round, row-streamed too — each node's
@@ -775,7 +783,7 @@ def next_step(state, params, rundir):
     defer = False
     if weng is not None:
         _last_round.clear()
-        _last_round[id(active)] = weng
+        _last_round[id(active)] = weakref.ref(weng)
     if not sample:
         if feng is not None:
             t0 = clock()
