@@ -192,8 +192,10 @@ _no_device_step = {}
 def _device_step_ok(params, nodes):
     """The plain round's optimizer step may run on the device (_FusedEngine(plain=True)): every
     node's optimizer is the plugin's plain SGD (optimizer() above, momentum 0: no state, p += -lr g)
-    over exactly its model's parameters, at params' learning rate; NIIDMIX_DEVICE_STEP=0 disables
-    it (the CPU steps, as rounds 1-5 did)."""
+    over exactly its model's parameters, all trainable, at params' learning rate;
+    NIIDMIX_DEVICE_STEP=0 disables it (the CPU steps, as rounds 1-5 did).  The device steps every
+    parameter: one the forward does not use (its gradient stays the -0.0 fill, where torch leaves
+    None and the optimizer skips it) ends the step unchanged except that a -0.0 becomes +0.0."""
     if os.environ.get("NIIDMIX_DEVICE_STEP", "1") == "0" or not _resident_ok():
         return False
     hit = _no_device_step.get(id(nodes))
@@ -214,6 +216,8 @@ def _device_step_ok(params, nodes):
                 mine = list(nd["model"].parameters())
             if len(g["params"]) != len(mine) or any(a is not b for a, b in zip(g["params"], mine)):
                 return False
+            if not all(q.requires_grad for q in mine):     # a frozen parameter gets no gradient:
+                return False                               # the CPU optimizer skips it
             _sgd_checked[opt] = weakref.ref(nd["model"])
     return True
 

@@ -355,6 +355,9 @@ def test_device_step_eligibility(monkeypatch):
     nd = nodes_with()
     nd[2]["optimizer"] = torch.optim.Adam(nd[2]["model"].parameters(), lr=0.1)
     assert not d_sgd._device_step_ok(params, nd)
+    nd = nodes_with()
+    nd[0]["model"].bias.requires_grad_(False)
+    assert not d_sgd._device_step_ok(params, nd)          # a frozen parameter
     monkeypatch.setenv("NIIDMIX_DEVICE_STEP", "0")
     assert not d_sgd._device_step_ok(params, nodes_with())
     monkeypatch.delenv("NIIDMIX_DEVICE_STEP")
