@@ -268,7 +268,7 @@ int niidmix_mix_tile_f32(const float *x, int64_t ld_x, float *y, int64_t ld_y, i
  *                (| NIIDMIX_TILE_POS_UNIFORM as for niidmix_tile_plan.pos_src)
  *   sub_slot     [n_sub*rt] int32 index of each tile row's own row in the group list (0 for unused)
  *   n_grp        groups;  grp_tile_ptr [n_grp+1] int32 tile ranges;  max_tiles = most tiles in a
- *                group: 1..16 for rt 8, 1..8 for rt 16, 1..4 for rt 32 (64*max_tiles threads)
+ *                group: 1..16 for rt 8, 1..12 for rt 16, 1..4 for rt 32 (64*max_tiles threads)
  *   grp_src_ptr  [n_grp+1] int32;  grp_src_rows  int32 source rows;  max_src = largest list (<= 256:
  *                max_src * 512 B of LDS)
  * Needs even p and ld and 8-B aligned slabs (2 columns per lane).  mode as niidmix_mix_tile_f32. */

@@ -2988,7 +2988,9 @@ inline size_t tlds_slack(bool seg, int cw) {
     const size_t spare = seg ? 2 * (size_t)cw * sizeof(float) : 0;
     return NIIDMIX_TLDS_GLDS && spare < 1024 ? 1024 - spare : 0;
 }
-constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 8 : 4; }
+// rt 16: up to 12 tiles per group, so a clique cut into shorter tiles (niidmix.tile: tile rows per
+// plan) gets more waves per block where the VGPR budget leaves room for them
+constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 12 : 4; }
 
 template <bool B> struct BoolC { static constexpr bool value = B; };
 

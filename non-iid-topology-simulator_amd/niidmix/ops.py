@@ -32,8 +32,8 @@ import torch
 
 from . import _lib
 from .factor import build_clique_plan
-from .tile import (LDS_MAX_WAVES, build_tile_lds_plan, build_tile_mfma_positions, build_tile_plan,
-                   build_tile_segments)
+from .tile import (LDS_MAX_WAVES, balanced_tile_rows, build_tile_lds_plan, build_tile_mfma_positions,
+                   build_tile_plan, build_tile_segments)
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -686,8 +686,13 @@ class Mixer:
             if not grp:
                 span = rt * LDS_MAX_WAVES.get(rt, 1)
                 grp = [list(range(s, min(s + span, csr.n))) for s in range(0, csr.n, span)]
+            # rows per rt-16 tile: balanced_tile_rows (an even wave count per SIMD);
+            # NIIDMIX_TILE_LDS_ROWS fixes it (tuning A/B)
+            trows = os.environ.get("NIIDMIX_TILE_LDS_ROWS", "auto")
+            trows = (self._hosted(("tlds_rows", rt), lambda: balanced_tile_rows(csr, grp, rt))
+                     if trows == "auto" else int(trows))
             self.tlds, self.tlds_reason = self._hosted(
-                ("tlds", rt), lambda: build_tile_lds_plan(csr, grp, rt))
+                ("tlds", rt, trows), lambda: build_tile_lds_plan(csr, grp, rt, tile_rows=trows))
             # register rows for sources outside a group that only masked entries read (a gateway
             # row's inter-clique neighbour): the stage shrinks to the group's own rows (10 000
             # d-cliques nodes: 199 staged rows -> 100, 128-column items instead of 96; 1000 nodes:
@@ -699,12 +704,13 @@ class Mixer:
             rem = os.environ.get("NIIDMIX_TLDS_REMOTE", "auto")
             lp0 = self.tlds
             if lp0 is not None and rt == 16 and rem != "0":
-                lr, _ = self._hosted(("tlds_rem", rt),
-                                     lambda: build_tile_lds_plan(csr, grp, rt, remote_regs=True))
+                lr, _ = self._hosted(("tlds_rem", rt, trows),
+                                     lambda: build_tile_lds_plan(csr, grp, rt, remote_regs=True,
+                                                                 tile_rows=trows))
                 if lr is not None and lr.rem_rows is not None and lr.rem_regs == 16 and rem != "16" \
                         and (rem == "8" or self._rem8_fits(lr)):
-                    l8, _ = self._hosted(("tlds_rem8", rt), lambda: build_tile_lds_plan(
-                        csr, grp, rt, remote_regs=True, rem_cap=8))
+                    l8, _ = self._hosted(("tlds_rem8", rt, trows), lambda: build_tile_lds_plan(
+                        csr, grp, rt, remote_regs=True, rem_cap=8, tile_rows=trows))
                     if l8 is not None and l8.rem_rows is not None:
                         lr = l8
                 if lr is not None and lr.rem_rows is not None:

@@ -242,7 +242,8 @@ def build_tile_plan(csr, groups=None, rt=16, max_rows=None):
 
 
 LDS_MAX_SRC = 256
-LDS_MAX_WAVES = {8: 16, 16: 8, 32: 4}
+LDS_MAX_WAVES = {8: 16, 16: 8, 32: 4}     # waves (tiles) of a block: the span of row groups
+MAX_TILES = {8: 16, 16: 12, 32: 4}        # tiles a group may have (k_mix_tile_lds launch bounds)
 POS_REMOTE = 1 << 29           # pos_slot flag: the source is one of the tile's register rows
 REM_MAX = 16                   # register rows per tile (rem_rows[t * REM_MAX + i])
 
@@ -305,12 +306,35 @@ def _register_sources(tp, t0, t1, srcs, members, row_mask, cap=None):
     return per_tile
 
 
-def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False, rem_cap=REM_MAX):
+def balanced_tile_rows(csr, groups, rt=16):
+    """Rows per rt-16 tile for k_mix_tile_lds: 16, unless the groups cut into 4k - 1 tiles (a
+    100-row clique: 7), whose block then leaves one of the CU's four SIMDs a wave short in every
+    block (7 waves: 2, 2, 2, 1): then the largest height that cuts one tile more (8 waves, two per
+    SIMD; 1000-node d-cliques: 13-row tiles, three blocks x 8 waves = the 6 waves per SIMD its 80
+    VGPRs allow).  Same box, headline exact round: 2.75 vs 2.81 ms (profiles/r06/tile_rows/)."""
+    if rt != 16 or not groups:
+        return rt
+    rp, col, val = csr.row_ptr, csr.col, csr.val
+    tiles = lambda r: max(len(_class_tiles(g, rp, col, val, rt, r)) for g in groups)
+    t16 = tiles(rt)
+    if t16 % 4 != 3 or t16 + 1 > MAX_TILES[rt]:
+        return rt
+    for r in range(rt - 1, rt // 2, -1):
+        t = tiles(r)
+        if t == t16 + 1:
+            return r
+        if t > t16 + 1:
+            break
+    return rt
+
+
+def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False, rem_cap=REM_MAX, tile_rows=None):
     """(plan, None) or (None, reason): build_tile_plan over `groups`, then per group the sorted list
     of distinct source rows (every row its tiles read, self rows included) and the slot indices.
     remote_regs (RT 16, segment walker only): sources outside a group that only MASKED entries
     read (_register_sources) are loaded into registers per tile (rem_rows) instead of staged, at
-    most rem_cap (8 or 16) per tile; the rest stay staged."""
+    most rem_cap (8 or 16) per tile; the rest stay staged.  tile_rows (RT 16): at most that many
+    rows per tile (more, shorter tiles: more waves per block, up to MAX_TILES)."""
     if rem_cap not in (8, REM_MAX):
         raise ValueError(f"rem_cap {rem_cap} (8 or {REM_MAX})")
     if rt not in LDS_MAX_WAVES:
@@ -333,7 +357,9 @@ def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False, rem_cap=REM_M
     # pad: full-height tiles, one tile fewer per 1000-node d-clique (7 instead of 8).
     pad_default = "0" if rt == 16 else "1"
     max_rows = rt - 1 if os.environ.get("NIIDMIX_TILE_LDS_PAD", pad_default) == "1" else rt
-    if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.col, csr.val, rt, max_rows)) > LDS_MAX_WAVES[rt]
+    if rt == 16 and tile_rows is not None:
+        max_rows = min(max_rows, int(tile_rows))
+    if max_rows < rt and groups and any(len(_class_tiles(g, csr.row_ptr, csr.col, csr.val, rt, max_rows)) > MAX_TILES[rt]
                       for g in groups):
         max_rows = rt
     tp, why = build_tile_plan(csr, groups, rt, max_rows)
@@ -369,8 +395,8 @@ def build_tile_lds_plan(csr, groups=None, rt=8, remote_regs=False, rem_cap=REM_M
             srcs = np.asarray([v for v in srcs if int(v) not in in_regs], srcs.dtype)
         if len(srcs) > LDS_MAX_SRC:
             return None, f"group {gi} reads {len(srcs)} distinct rows (> {LDS_MAX_SRC})"
-        if t1 - t0 > LDS_MAX_WAVES[rt]:
-            return None, f"group {gi} has {t1 - t0} tiles of {rt} rows (> {LDS_MAX_WAVES[rt]})"
+        if t1 - t0 > MAX_TILES[rt]:
+            return None, f"group {gi} has {t1 - t0} tiles of {rt} rows (> {MAX_TILES[rt]})"
         slot_of = {int(r): i for i, r in enumerate(srcs)}
         for t in range(t0, t1):
             for k in range(int(tp.sub_ptr[t]), int(tp.sub_ptr[t + 1])):

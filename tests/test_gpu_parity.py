@@ -761,6 +761,32 @@ def test_tile_lds_register_rows_vs_golden(name, mode, regs, gpu, oracle_mod, mon
         assert ok, (name, worst)
 
 
+@pytest.mark.parametrize("rows", ["auto", "13", "10", "9"])
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("name", golden_cases("dcliques"))
+def test_tile_lds_tile_rows_vs_golden(name, mode, rows, gpu, oracle_mod, monkeypatch):
+    """Shorter rt-16 tiles (NIIDMIX_TILE_LDS_ROWS; "auto" = tile.balanced_tile_rows, the default):
+    more tiles -- waves -- per group, up to 12, with the register-row plans and the 9..15-row
+    walker loops: bitwise the reference in exact mode, within the tolerance in fast mode."""
+    g = load_golden(name)
+    if g["x"].shape[1] % 2:
+        pytest.skip("odd p: the LDS tile kernel reads column pairs")
+    monkeypatch.setenv("NIIDMIX_TILE_LDS_ROWS", rows)
+    m = _mixer(g, gpu)
+    if m.tlds is None:
+        pytest.skip(m.tlds_reason)
+    if rows != "auto":
+        assert int(np.max(m.tlds.tile.sub_rows.reshape(-1, 16) >= 0, axis=0).sum()) <= int(rows)
+    x = torch.from_numpy(g["x"]).to(gpu)
+    y = m(x, kernel="tile-lds-" + mode).cpu().numpy()
+    if mode == "exact":
+        assert oracle_mod.bitwise_equal(y, g["y"]), name
+    else:
+        bound = oracle_mod.condition_bound(g["x"], g["row_ptr"], g["col"], g["val"])
+        ok, worst = oracle_mod.check_tolerance(y, g["y"], bound, rtol=RTOL)
+        assert ok, (name, worst)
+
+
 @pytest.mark.parametrize("n,p", [(1000, 4096 + 12), (64, 33), (130, 257), (257, 1030), (17, 5)])
 def test_dense_b6_split_gemm(n, p, gpu, oracle_mod):
     """The bf16x6 dense GEMM (kernel "dense": three-term bf16 splits, six products on

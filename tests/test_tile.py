@@ -216,6 +216,31 @@ def test_register_rows_apply_csr_rows(name, cap):
     _assert_rows_are_csr(tile.segments_row_lists(lp, ts), csr)
 
 
+def test_balanced_tile_rows_dcliques():
+    """balanced_tile_rows: a 100-row clique cuts into 7 full-height tiles (4k - 1 waves: one SIMD a
+    wave short), so the rule picks the tallest height that cuts 8; the plan then has 8 tiles per
+    clique, none taller than that height, and the segment walker's view still gives every row
+    its CSR row in order (with and without register rows)."""
+    from niidmix import tile
+    g = load_golden("dcliques1000_fc_p64")
+    csr = _csr(g).validate()
+    r = tile.balanced_tile_rows(csr, g["cliques"], 16)
+    assert 8 < r < 16
+    for remote in (False, True):
+        lp, why = tile.build_tile_lds_plan(csr, g["cliques"], 16, remote_regs=remote, tile_rows=r)
+        assert lp is not None, why
+        assert lp.max_tiles == 8 and lp.tile.n_sub == 80
+        assert int((lp.tile.sub_rows.reshape(-1, 16) >= 0).sum(1).max()) <= r
+        _assert_rows_are_csr(tile.segments_row_lists(lp, tile.build_tile_segments(lp)), csr)
+    # already a multiple of 4 (or not rt 16): unchanged
+    assert tile.balanced_tile_rows(csr, [c[:64] for c in g["cliques"]] +
+                                   [c[64:] for c in g["cliques"]], 16) == 16
+    assert tile.balanced_tile_rows(csr, g["cliques"], 8) == 8
+    # a height that would cut more tiles than a block may have (8 rows: 13): full-height tiles
+    lp, why = tile.build_tile_lds_plan(csr, g["cliques"], 16, tile_rows=8)
+    assert lp is not None and lp.max_tiles == 7, why
+
+
 def test_register_rows_cap_argument():
     from niidmix import tile
     g = load_golden("dcliques1000_fc_p64")
