@@ -310,7 +310,10 @@ typedef struct niidmix_tile_lds_plan {
      * reads register row (word 0 & 0xfff).  Round 4 (ABI 4). */
     const int32_t *rem_rows;
     /* register rows the kernel loads per tile: 8 (every tile's rem_rows entries 8..15 are -1; 16
-     * fewer VGPRs, so three 7-wave blocks fit a CU) or 16; 0 = 16 */
+     * fewer VGPRs, so three 7-wave blocks fit a CU) or 16; 0 = 16; -16: all 16 in two phases of 8
+     * in the 8-row kernel's registers, 8..15 loaded when the walk reaches the first segment that
+     * reads one -- only for plans whose tiles read rows 0..7 before any of 8..15
+     * (niidmix.tile.rem_two_phase) */
     int32_t rem_regs;
 } niidmix_tile_lds_plan;
 

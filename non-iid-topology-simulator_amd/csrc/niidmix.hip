@@ -2690,10 +2690,13 @@ __device__ __forceinline__ void tlds16_run(Acc16 &acc, int j, int stop, int v_me
 // REGISTER rows (plans with rem_rows): a masked entry whose word 0 has bit 29 set takes its source
 // from the tile's register rows, pinned in v[64:95] (register row i in v[64 + 2i : 65 + 2i]),
 // picked by GPR-index mode, instead of from the LDS stage.
-#define NIIDMIX_SEG_REMOTE                                                                           \
+#define NIIDMIX_SEG_REMOTE NIIDMIX_SEG_REMOTE_M("0xfff")
+// 8 register rows: index & 7 (the two-phase kernel walks rows 8..15 of a 16-row plan in v[64:79])
+#define NIIDMIX_SEG_REMOTE8 NIIDMIX_SEG_REMOTE_M("7")
+#define NIIDMIX_SEG_REMOTE_M(MASK)                                                                   \
     "s_bitcmp1_b32 s41, 29\n\t"                                                                     \
     "s_cbranch_scc0 .Lw_lds_%=\n\t"                                                                 \
-    "s_and_b32 s46, s41, 0xfff\n\t"                                                                 \
+    "s_and_b32 s46, s41, " MASK "\n\t"                                                              \
     "s_lshl_b32 s46, s46, 1\n\t"                                                                    \
     "s_set_gpr_idx_on s46, gpr_idx(SRC0)\n\t"                                                       \
     "v_mov_b32 %[q0], v64\n\t"                                                                      \
@@ -2836,9 +2839,9 @@ __device__ __forceinline__ void tlds16_walk_rem(Acc16 &acc, const int32_t *segp,
     else if constexpr (NREM == 16)
         NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN);
     else if constexpr (EXACT)
-        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
+        NIIDMIX_SEG_WALK_X(NIIDMIX_SEG_UPD_EXACT, NIIDMIX_MSK_EXACT, NIIDMIX_SEG_REMOTE8, NIIDMIX_REM_IN8);
     else
-        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE, NIIDMIX_REM_IN8);
+        NIIDMIX_SEG_WALK_X(NIIDMIX_UPD_FAST, NIIDMIX_MSK_FAST, NIIDMIX_SEG_REMOTE8, NIIDMIX_REM_IN8);
     (void)pr;
 }
 
@@ -2994,7 +2997,9 @@ constexpr int tile_lds_max_waves(int rt) { return rt == 8 ? 16 : rt == 16 ? 12 :
 
 template <bool B> struct BoolC { static constexpr bool value = B; };
 
-template <bool EXACT, int RT, int SV, int RS, bool SEG, int NREM = 0, bool MF = false>
+// REM2 (NREM 8): the plan has up to 16 register rows per tile, walked in two phases of 8 (rows
+// 0..7 loaded before the walk, 8..15 once the walk reaches the first segment that reads one)
+template <bool EXACT, int RT, int SV, int RS, bool SEG, int NREM = 0, bool MF = false, bool REM2 = false>
 __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
     int64_t n_grp, const int32_t *__restrict__ grp_tile_ptr, const int32_t *__restrict__ grp_src_ptr,
@@ -3390,7 +3395,33 @@ __global__ __launch_bounds__(64 * tile_lds_max_waves(RT)) void k_mix_tile_lds(
                 // it, its weight (fp32 bits).  One walker for every tile: walkers specialised by the
                 // tile's row count (4 / 8 / 12 / 16 pairs) measured no faster, and their four call
                 // sites made hipcc keep a second copy of the tuple (90 VGPRs, two blocks per CU)
-                if constexpr (REM)
+                if constexpr (REM && REM2) {
+                    // two phases: the first segment reading register row 8..15 (a masked entry
+                    // with SEG_REMOTE and index >= 8; the plan reads rows 0..7 only before it,
+                    // niidmix.tile.rem_two_phase) splits the walk; rows 8..15 replace 0..7 there
+                    int sm = sb1;
+                    for (int b = sb0; b < sb1; b += kWave) {
+                        const int i = b + lane;
+                        const int dx = i < sb1 ? seg[4 * i] : 0;
+                        const uint64_t hit = __ballot((dx & (3 << 29)) == (3 << 29) && (dx & 0xfff) >= 8);
+                        if (hit) { sm = b + __builtin_ctzll(hit); break; }
+                    }
+                    tlds16_walk_rem<EXACT, rs * (int)sizeof(f2), 8>(acc.v[0], seg, sb0, sm, (int)lds_base,
+                                                                     w0, w1, lane8, lane, nr, rem);
+                    if (sm < sb1) {
+                        const int sl_ = lane < rs ? lane : rs - 1;
+                        const int64_t cr = c0 + 2 * sl_ < p ? c0 + 2 * sl_ : c0;
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const int row = rem_rows[sub * 16 + 8 + r];
+                            const f2 v = *reinterpret_cast<const f2 *>(x + (int64_t)(row < 0 ? 0 : row) * ld_x + cr);
+                            rem[2 * r] = v.x;
+                            rem[2 * r + 1] = v.y;
+                        }
+                        tlds16_walk_rem<EXACT, rs * (int)sizeof(f2), 8>(acc.v[0], seg, sm, sb1, (int)lds_base,
+                                                                         w0, w1, lane8, lane, nr, rem);
+                    }
+                } else if constexpr (REM)
                     tlds16_walk_rem<EXACT, rs * (int)sizeof(f2), (NREM ? NREM : 16)>(acc.v[0], seg, sb0, sb1, (int)lds_base, w0,
                                                                  w1, lane8, lane, nr, rem);
                 else
@@ -4562,9 +4593,12 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     const bool rem = plan->rem_rows != nullptr;
     if (rem && (!seg || plan->mf_ptr != nullptr))
         return set_error(NIIDMIX_EINVAL, "rem_rows needs the segment walker (seg_ptr set, mf_ptr NULL)");
-    if (rem && plan->rem_regs != 0 && plan->rem_regs != 8 && plan->rem_regs != 16)
-        return set_error(NIIDMIX_EINVAL, "rem_regs %d (0, 8 or 16)", plan->rem_regs);
+    if (rem && plan->rem_regs != 0 && plan->rem_regs != 8 && plan->rem_regs != 16 && plan->rem_regs != -16)
+        return set_error(NIIDMIX_EINVAL, "rem_regs %d (0, 8, 16 or -16)", plan->rem_regs);
     const bool rem8 = rem && plan->rem_regs == 8;
+    // -16: up to 16 register rows walked in two phases of 8 (80 VGPRs instead of 96); the host
+    // sets it only for plans whose tiles read rows 0..7 before any of 8..15 (tile.rem_two_phase)
+    const bool rem2 = rem && plan->rem_regs == -16;
     if (mf && !plan->mf) return set_error(NIIDMIX_EINVAL, "null MFMA position list");
     // waves of a block on the matrix cores (the rest walk segments on the VALU side by side);
     // NIIDMIX_TLDS_MF_WAVES overrides (tuning), default every wave
@@ -4590,9 +4624,11 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
     if (n_items > 0x7fffffffLL) return set_error(NIIDMIX_EUNSUPPORTED, "too many (group, chunk) items");
     const size_t lds = (size_t)stage_rows * cw * sizeof(float) + tlds_slack(seg, cw);
     const dim3 grid((unsigned)n_items), block((unsigned)(64 * plan->max_tiles));
-#define NIIDMIX_TLDS_CW(E, R, V, SG, RM, M) (cw == 120 ? k_mix_tile_lds<E, R, V, 60, SG, RM, M> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, SG, RM, M> : k_mix_tile_lds<E, R, V, 64, SG, RM, M>)
+#define NIIDMIX_TLDS_CW2(E, R, V, SG, RM, M, R2) (cw == 120 ? k_mix_tile_lds<E, R, V, 60, SG, RM, M, R2> : cw == 96 ? k_mix_tile_lds<E, R, V, 48, SG, RM, M, R2> : k_mix_tile_lds<E, R, V, 64, SG, RM, M, R2>)
+#define NIIDMIX_TLDS_CW(E, R, V, SG, RM, M) NIIDMIX_TLDS_CW2(E, R, V, SG, RM, M, false)
 #define NIIDMIX_TLDS(E, R, V) do { \
         auto kfn = seg ? (rem ? (rem8 ? NIIDMIX_TLDS_CW(E, R, V, (R == 16), (R == 16 ? 8 : 0), false) \
+                                : rem2 ? NIIDMIX_TLDS_CW2(E, R, V, (R == 16), (R == 16 ? 8 : 0), false, (R == 16)) \
                                      : NIIDMIX_TLDS_CW(E, R, V, (R == 16), (R == 16 ? 16 : 0), false)) \
                               : mf ? NIIDMIX_TLDS_CW(E, R, V, (R == 16), 0, (E && R == 16)) \
                                    : NIIDMIX_TLDS_CW(E, R, V, (R == 16), 0, false)) \
@@ -4608,6 +4644,7 @@ int niidmix_mix_tile_lds_f32(const float *x, int64_t ld_x, float *y, int64_t ld_
 #undef NIIDMIX_TLDS_V
 #undef NIIDMIX_TLDS
 #undef NIIDMIX_TLDS_CW
+#undef NIIDMIX_TLDS_CW2
     return check_launch("k_mix_tile_lds");
 }
 

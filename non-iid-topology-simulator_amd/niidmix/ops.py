@@ -33,7 +33,7 @@ import torch
 from . import _lib
 from .factor import build_clique_plan
 from .tile import (LDS_MAX_WAVES, balanced_tile_rows, build_tile_lds_plan, build_tile_mfma_positions,
-                   build_tile_plan, build_tile_segments)
+                   build_tile_plan, build_tile_segments, rem_two_phase)
 from .topology import MixCSR, to_csr
 
 EXACT, FAST = _lib.MODE_EXACT, _lib.MODE_FAST
@@ -354,7 +354,7 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
     segments, exact mode): the matrix-core path, bit-identical, the walker its per-block fallback.
     rem_rows: the plan's register rows (build_tile_lds_plan(remote_regs=True); segments only);
     rem_regs: how many of each tile's 16 entries the kernel loads (8 when no tile has more, else 16;
-    TileLdsPlan.rem_regs)."""
+    TileLdsPlan.rem_regs), or -16: all 16 in two phases of 8 (tile.rem_two_phase plans only)."""
     _slab("x", x)
     _slab("out", out, cols=x.shape[1])
     dev = x.device
@@ -391,7 +391,7 @@ def mix_tile_lds(x: torch.Tensor, sub_ptr: torch.Tensor, sub_rows: torch.Tensor,
         _req(seg_ptr is not None and mf_ptr is None,
              "register rows: with the segments and without the MFMA position lists")
         _vec("rem_rows", rem_rows, torch.int32, dev, t * 16)       # rows < x.shape[0]: the plan's
-        _req(rem_regs in (8, 16), f"rem_regs {rem_regs} (8 or 16)")
+        _req(rem_regs in (8, 16, -16), f"rem_regs {rem_regs} (8, 16 or -16)")
         rem = rem_rows.data_ptr()
     _no_overlap(x, out)
     some = sub_ptr.data_ptr()
@@ -550,7 +550,7 @@ _LAZY = {
     "l_sub_slot": "tlds", "l_sub_wself": "tlds", "l_pos_slot": "tlds", "l_pos_mask": "tlds",
     "l_pos_w": "tlds", "l_grp_tile_ptr": "tlds", "l_grp_src_ptr": "tlds", "l_grp_src_rows": "tlds",
     "tseg": "tlds", "s_seg_ptr": "tlds", "s_seg": "tlds", "s_seg_w": "tlds",
-    "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds", "l_rem_rows": "tlds",
+    "tmf": "tlds", "m_mf_ptr": "tlds", "m_mf": "tlds", "l_rem_rows": "tlds", "tlds_rem2": "tlds",
     "w_dense": "dense", "w_split": "dense",
     "ell": "ell", "e_col": "ell", "e_val": "ell", "e_len": "ell", "band": "ell",
 }
@@ -766,6 +766,9 @@ class Mixer:
             self.s_seg_w = torch.from_numpy(np.ascontiguousarray(ts.seg_w).reshape(-1)).to(dev)
         self.l_rem_rows = (torch.from_numpy(lp.rem_rows).to(dev) if lp.rem_rows is not None
                            else None)
+        # 16 register rows walked in two phases of 8 (80 VGPRs: as many blocks per CU as the LDS
+        # allows instead of two)
+        self.tlds_rem2 = lp.rem_regs == 16 and ts is not None and rem_two_phase(lp, ts)
         self.tmf = tm if ts is not None else None
         if self.tmf is not None:
             self.m_mf_ptr = torch.from_numpy(tm.mf_ptr).to(dev)
@@ -941,7 +944,11 @@ class Mixer:
                     self.tmf is not None and self.tmf.lp is lp:
                 segs = segs + (self.m_mf_ptr, self.m_mf)
             if rem is not None:
-                segs = segs + (None, None, rem, lp.rem_regs)
+                # two phases of 8 register rows (80 VGPRs: three 8-wave blocks per CU instead of
+                # two) where the plan allows it; 10 000 nodes 31.3 vs 32.4 ms
+                # (profiles/r06/tile_rows/); NIIDMIX_TLDS_REM2=0: the 16-register kernel
+                two = self.tlds_rem2 and os.environ.get("NIIDMIX_TLDS_REM2", "1") == "1"
+                segs = segs + (None, None, rem, -16 if two else lp.rem_regs)
             mix_tile_lds(x, self.l_sub_ptr, self.l_sub_rows, self.l_sub_slot, self.l_sub_wself,
                          self.l_pos_slot, self.l_pos_mask, self.l_pos_w, self.l_grp_tile_ptr,
                          self.l_grp_src_ptr, self.l_grp_src_rows, out, lp.tile.rt, lp.max_src,

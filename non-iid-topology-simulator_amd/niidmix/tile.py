@@ -567,6 +567,26 @@ def build_tile_segments(lp, max_len=32):
                         seg_w=np.asarray(seg_w, np.float32).reshape(-1, 2), lp=lp)
 
 
+def rem_two_phase(lp, ts):
+    """May k_mix_tile_lds walk this plan's register rows in two phases of 8 (rem_regs -16: 80 VGPRs
+    instead of 96)?  Every tile must read register rows 0..7 only before its first segment that
+    reads one of 8..15: the kernel loads 0..7 before the walk and 8..15 into the same registers
+    there.  rem_rows lists a tile's register rows in first-use order and each is read by one
+    masked entry, so d-cliques plans qualify."""
+    if lp.rem_rows is None or ts is None or ts.lp is not lp:
+        return False
+    w0 = np.asarray(ts.seg)[:, 0].astype(np.int64)
+    rem = ((w0 & SEG_HARD) != 0) & ((w0 & SEG_REMOTE) != 0)
+    high = rem & ((w0 & SEG_SLOT) >= 8)
+    low = rem & ((w0 & SEG_SLOT) < 8)
+    for t in range(lp.tile.n_sub):
+        b, e = int(ts.seg_ptr[t]), int(ts.seg_ptr[t + 1])
+        h = np.flatnonzero(high[b:e])
+        if len(h) and np.any(low[b + h[0]:e]):
+            return False
+    return True
+
+
 def segments_row_lists(lp, ts):
     """{row: [(src, w), ...]} as the segment loop applies them (self first) -- for checks."""
     tp = lp.tile

@@ -269,6 +269,46 @@ def test_tile_lds_segment_loop_masked_heavy(n, size, inter, gpu, oracle_mod):
     assert oracle_mod.bitwise_equal(y, ref), (n, size, inter)
 
 
+@pytest.mark.parametrize("p", [1002, 256])
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("two", ["1", "0"])
+@pytest.mark.parametrize("n", [2000, 3000])
+def test_tile_lds_register_rows_two_phase(n, two, mode, p, gpu, oracle_mod, monkeypatch):
+    """16 register rows per tile walked in two phases of 8 (rem_regs -16, NIIDMIX_TLDS_REM2):
+    d-cliques of 100 with 20 / 30 cliques put 10-15 gateway rows -- register rows -- in a tile,
+    so the walk reloads rows 8..15 mid-tile.  Exact: bitwise the C oracle, with -0.0, a
+    subnormal and inf / NaN in register rows (they reach only the rows reading them); fast:
+    within the tolerance.  two = "0": the 16-register kernel on the same plan."""
+    from niidmix.generate import dcliques_csr
+    monkeypatch.setenv("NIIDMIX_TLDS_REM2", two)
+    csr, cl = dcliques_csr(n, 100, "fully-connected", 1337)
+    g = {"row_ptr": csr.row_ptr, "col": csr.col, "val": csr.val, "cliques": cl}
+    m = _mixer(g, gpu)
+    lp = m.tlds
+    assert lp is not None and lp.rem_rows is not None and lp.rem_regs == 16 and m.tlds_rem2
+    assert int((lp.rem_rows.reshape(-1, 16) >= 0).sum(1).max()) > 8
+    x = np.random.default_rng(n + p).standard_normal((n, p)).astype(np.float32)
+    regs = np.unique(lp.rem_rows[lp.rem_rows >= 0])
+    x[regs[0], 3] = -0.0
+    x[regs[1], 5] = np.float32(1e-42)
+    if mode == "exact":
+        x[regs[-1], 7] = np.inf
+        x[regs[-2], 9] = np.nan
+    y = m(torch.from_numpy(x).to(gpu), kernel="tile-lds-" + mode).cpu().numpy()
+    ref = oracle_mod.mix_exact_c(x, csr.row_ptr, csr.col, csr.val)
+    if mode == "exact":
+        assert oracle_mod.bitwise_equal(y, ref), (n, two)
+        # every reader of the register row (its clique and its remote gateway) and no other; the
+        # row's own output is NaN (x_self * 0)
+        assert (~np.isfinite(y[:, 7])).sum() == (csr.col == regs[-1]).sum()
+        assert np.isnan(y[regs[-1], 7]) and np.isinf(y[:, 7]).sum() == (csr.col == regs[-1]).sum() - 1
+        assert np.isnan(y[:, 9]).sum() == (csr.col == regs[-2]).sum()
+    else:
+        bound = oracle_mod.condition_bound(x, csr.row_ptr, csr.col, csr.val)
+        ok, worst = oracle_mod.check_tolerance(y, ref, bound, rtol=RTOL)
+        assert ok, (n, two, worst)
+
+
 @pytest.mark.parametrize("remote", ["0", "auto"])
 def test_tile_lds_narrow_items_float2(remote, gpu, oracle_mod, monkeypatch):
     """The all-staged 1000-node d-cliques plan picks 120-column items by itself (109 staged
