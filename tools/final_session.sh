@@ -6,14 +6,18 @@
 #   tools/final_session.sh NAME cfgB      10 000 nodes (fast, exact), dense bf16x6, dense fp32
 #   tools/final_session.sh NAME e2e       the host-resident round (bench.py --e2e --e2e-step)
 #
+#   tools/final_session.sh NAME merge     (here, after the parts) stamps of every part -> profiles/traffic.json
+#
 # Per config: a bench line, a kernel trace (--stats) and two separate PMC passes (FETCH_SIZE,
-# WRITE_SIZE) whose per-launch bytes are stamped with the library hash into $O/traffic.json (seeded
-# from profiles/traffic.json; copy it back by hand).  Every GPU step has its own time limit; a step
-# that fails ends the session.
+# WRITE_SIZE) whose per-launch bytes are stamped with the library hash into $O/traffic_PART.json
+# (seeded from profiles/traffic.json: each part runs on a fresh box, and one file per part keeps a
+# later part's merge from overwriting an earlier part's stamps).  Every GPU step has its own time
+# limit; a step that fails ends the session.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"
 O=gpurun_out/${1:-final}; PART=${2:-tests}; mkdir -p $O; export TMPDIR=/tmp
-[ -f $O/traffic.json ] || cp profiles/traffic.json $O/traffic.json
+T=$O/traffic_$PART.json
+[ "$PART" = merge ] || [ -f $T ] || cp profiles/traffic.json $T
 one() {   # name kernel-substring alg-bytes bench-args...
   n=$1; k=$2; alg=$3; shift 3
   timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench $n failed"; tail -5 $O/bench_$n.err; return 1; }
@@ -21,7 +25,7 @@ one() {   # name kernel-substring alg-bytes bench-args...
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/$O/pmc_${n}_$c -o p -- python3 $R/bench.py --no-cpu-baseline --no-cold-cache "$@" > $O/pmc_${n}_$c.log 2>&1 || { echo "pmc $n $c failed"; tail -5 $O/pmc_${n}_$c.log; return 1; }
   done
-  python tools/pmc_traffic.py $O/pmc_${n}_FETCH_SIZE $O/pmc_${n}_WRITE_SIZE $k --alg-bytes $alg --key-from $O/bench_$n.json --out $O/traffic.json > $O/traffic_$n.txt || return 1
+  python tools/pmc_traffic.py $O/pmc_${n}_FETCH_SIZE $O/pmc_${n}_WRITE_SIZE $k --alg-bytes $alg --key-from $O/bench_$n.json --out $T > $O/traffic_$n.txt || return 1
   python -c "import json;d=json.load(open('$O/bench_$n.json'));t=json.load(open('$O/traffic_$n.txt'));print('$n', d['ms_per_step'], 'ms', d['roofline']['frac'], 'traffic x', round(t['ratio_to_algorithmic'],4))"
 }
 case $PART in
@@ -47,6 +51,19 @@ case $PART in
   e2e)
     timeout -k 10 1000 python bench.py --no-cpu-baseline --e2e --e2e-step --steps 3 > $O/bench_e2e.json 2> $O/bench_e2e.err || { echo e2e failed; tail $O/bench_e2e.err; exit 6; }
     python -c "import json;d=json.load(open('$O/bench_e2e.json'));e=d['e2e']['next_step'];[print(k, v) for k, v in e.items() if isinstance(v, dict)]" ;;
+  merge)
+    python - "$O" <<'PY' || exit 7
+import glob, json, sys
+path = "profiles/traffic.json"
+out = json.load(open(path))
+for f in sorted(glob.glob(sys.argv[1] + "/traffic_*.json")):
+    for k, v in json.load(open(f))["entries"].items():
+        if v != out["entries"].get(k):          # measured by this part (the rest is its seed)
+            out["entries"][k] = v
+            print("stamped", v.get("lib_sha16"), k)
+json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+PY
+    ;;
   *) echo "unknown part $PART"; exit 2 ;;
 esac
 echo "part $PART done"
