@@ -241,6 +241,39 @@ def test_balanced_tile_rows_dcliques():
     assert lp is not None and lp.max_tiles == 7, why
 
 
+def test_rem_two_phase_eligibility():
+    """rem_two_phase: d-cliques plans with more than 8 register rows per tile read rows 0..7 before
+    any of 8..15 (rem_rows lists them in first-use order, one masked entry each); a plan whose
+    segments read a low row after a high one is refused; plans without register rows too."""
+    import copy
+    from niidmix import tile
+    from niidmix.generate import dcliques_csr
+    csr, cl = dcliques_csr(2000, 100, "fully-connected", 1337)
+    lp, why = tile.build_tile_lds_plan(csr, cl, 16, remote_regs=True)
+    assert lp is not None, why
+    assert lp.rem_regs == 16 and int((lp.rem_rows.reshape(-1, 16) >= 0).sum(1).max()) > 8
+    ts = tile.build_tile_segments(lp)
+    assert tile.rem_two_phase(lp, ts)
+    _assert_rows_are_csr(tile.segments_row_lists(lp, ts), csr)
+    # swap the register indices 0 and 8 in the words of one tile that has both: 0 is then read last
+    w0 = ts.seg[:, 0].astype(np.int64)
+    remote = ((w0 & tile.SEG_HARD) != 0) & ((w0 & tile.SEG_REMOTE) != 0)
+    for t in range(lp.tile.n_sub):
+        b, e = int(ts.seg_ptr[t]), int(ts.seg_ptr[t + 1])
+        idx = {int(w0[k] & tile.SEG_SLOT): k for k in range(b, e) if remote[k]}
+        if 0 in idx and 8 in idx:
+            bad = copy.copy(ts)
+            bad.seg = ts.seg.copy()
+            bad.seg[idx[0], 0] = (bad.seg[idx[0], 0] & ~tile.SEG_SLOT) | 8
+            bad.seg[idx[8], 0] = (bad.seg[idx[8], 0] & ~tile.SEG_SLOT) | 0
+            assert not tile.rem_two_phase(lp, bad)
+            break
+    else:
+        raise AssertionError("no tile with register rows 0 and 8")
+    lp0, _ = tile.build_tile_lds_plan(csr, cl, 16)
+    assert not tile.rem_two_phase(lp0, tile.build_tile_segments(lp0))
+
+
 def test_register_rows_cap_argument():
     from niidmix import tile
     g = load_golden("dcliques1000_fc_p64")
