@@ -2075,6 +2075,156 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
     }
 }
 
+// (the item geometry shared by k_mix_bigclique_v4 and k_mix_bigclique_reg below)
+constexpr int kBigRegWaves = 16;
+constexpr int kBigRegCols = 32;
+// float4 lanes (round 6; launch_bigclique_reg picks it): the same item (clique, 32 columns) with
+// lane = (row r8 = lane >> 3, column quad q = lane & 7), so one wave-instruction loads / stores 8
+// member rows x 128 B = 1 KiB (k_mix_bigclique_reg: 2 rows x 128 B of 4-B lanes); wave w holds
+// members 8 (8 w + i) + r8, i < 8 (<= 1024 members).  Group sums: three xor-shuffles over r8, then
+// the 16 waves through LDS.  Same per-element arithmetic as k_mix_bigclique_reg (a x, then one fma
+// per group, then the residual fmas); the column sums are added in another order (fast mode).
+// Needs p % 4 == 0, ld % 4 == 0, 16-B aligned slabs, and column-blocked slabs whose blocks span
+// < 4 GiB (32-bit row offsets, as k_mix_clique_q's OFF32).
+template <int G, int OCC>
+__global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_mix_bigclique_v4(
+    const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
+    int32_t n_cliques, const int32_t *__restrict__ clique_ptr,
+    const int32_t *__restrict__ member_row, const int32_t *__restrict__ member_group,
+    const float *__restrict__ coef, const int32_t *__restrict__ res_ptr,
+    const int32_t *__restrict__ res_col, const float *__restrict__ res_val, int64_t nch8,
+    int bc_shift, int64_t bs_x, int64_t bs_y, int contig, const int64_t *__restrict__ csr_ptr,
+    const int32_t *__restrict__ csr_col, const float *__restrict__ csr_val) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int RI = 8;                                     // rows per lane
+    constexpr int MMAX = kBigRegWaves * 8 * RI;               // 1024
+    __shared__ int32_t s_row[MMAX];
+    __shared__ int32_t s_grp[MMAX];
+    __shared__ int32_t s_res[MMAX + 1];
+    __shared__ float s_cf[MMAX * (1 + G)];
+    __shared__ f4v red[G][kBigRegWaves][8];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int r8 = lane >> 3, q = lane & 7;
+    const int64_t n_items = (int64_t)n_cliques * nch8 * 8;
+    int32_t cur = -1, m0 = 0, M = 0;
+    for (int64_t t = blockIdx.x; t < n_items; t += gridDim.x) {
+        const int64_t xcd = t & 7;
+        const int64_t local = t >> 3;
+        const int32_t cq = (int32_t)(local / nch8);
+        const int64_t chunk = contig ? xcd * nch8 + local % nch8 : (local % nch8) * 8 + xcd;
+        const int64_t c0 = chunk * kBigRegCols;
+        if (c0 >= p) continue;                               // block-uniform
+        if (cq != cur) {                                     // block-uniform
+            __syncthreads();                                 // previous item done with s_*
+            cur = cq;
+            m0 = clique_ptr[cq];
+            M = clique_ptr[cq + 1] - m0;
+            for (int k = threadIdx.x; k < M; k += blockDim.x) {
+                s_row[k] = member_row[m0 + k];
+                s_grp[k] = member_group[m0 + k] & kMemberGroupMask;
+#pragma unroll
+                for (int g = 0; g <= G; ++g) s_cf[k * (1 + G) + g] = coef[(int64_t)(m0 + k) * (1 + G) + g];
+            }
+            for (int k = threadIdx.x; k <= M; k += blockDim.x) s_res[k] = res_ptr[m0 + k];
+            __syncthreads();
+        }
+        const bool act = c0 + 4 * q < p;                      // p % 4 == 0: a quad is all in or out
+        const unsigned lo = act ? (unsigned)(4 * q) : 0u;
+        const int64_t cin = c0 & (((int64_t)1 << bc_shift) - 1);
+        // column-blocked slabs only: the item's block base (wave-uniform) + a 32-bit row offset
+        const float *xb = x + (c0 >> bc_shift) * bs_x + cin;
+        float *yb = y + (c0 >> bc_shift) * bs_y + cin;
+        const float *xc = xb + lo;
+        f4v v[RI];
+#pragma unroll
+        for (int i = 0; i < RI; ++i) {
+            const int k = 8 * (wave * RI + i) + r8;
+            v[i] = k < M ? __builtin_nontemporal_load(reinterpret_cast<const f4v *>(qrow<true>(xb, s_row[k], ld_x, lo)))
+                         : f4v{0.f, 0.f, 0.f, 0.f};
+        }
+        f4v s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < RI; ++i) {
+            if (G == 1) {
+                s[0] += v[i];                                // rows past M hold 0
+            } else {
+                const int k = 8 * (wave * RI + i) + r8;
+                const int gr = k < M ? s_grp[k] : -1;
+#pragma unroll
+                for (int g = 0; g < G; ++g) s[g] += gr == g ? v[i] : f4v{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int m = 8; m < kWave; m <<= 1)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[g][e] += __shfl_xor(s[g][e], m);
+            if (r8 == 0) red[g][wave][q] = s[g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            f4v a = red[g][0][q];
+#pragma unroll
+            for (int w = 1; w < kBigRegWaves; ++w) a += red[g][w][q];
+            s[g] = a;
+        }
+        __syncthreads();                                      // red[] is rewritten by the next item
+#pragma unroll
+        for (int i = 0; i < RI; ++i) {
+            const int k = 8 * (wave * RI + i) + r8;
+            const float *cf = s_cf + (k < M ? k : 0) * (1 + G);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float o = cf[0] * v[i][e];
+#pragma unroll
+                for (int g = 0; g < G; ++g) o = __builtin_fmaf(cf[1 + g], s[g][e], o);
+                v[i][e] = o;
+            }
+        }
+        if (s_res[M] > s_res[0]) {                            // block-uniform: any gateway edges
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const int k = 8 * (wave * RI + i) + r8;
+                if (k < M)
+                    for (int32_t qq = s_res[k]; qq < s_res[k + 1]; ++qq) {
+                        const f4v xr = *reinterpret_cast<const f4v *>(qrow<true>(xb, res_col[qq], ld_x, lo));
+                        const float w = res_val[qq];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[i][e] = __builtin_fmaf(w, xr[e], v[i][e]);
+                    }
+            }
+        }
+        uint32_t bad = 0;                                     // this lane's rows with a non-finite output
+#pragma unroll
+        for (int i = 0; i < RI; ++i) {
+            const int k = 8 * (wave * RI + i) + r8;
+            if (k < M && act) {
+                const int rowk = s_row[k];
+                if (__builtin_isfinite(v[i][0]) && __builtin_isfinite(v[i][1]) &&
+                    __builtin_isfinite(v[i][2]) && __builtin_isfinite(v[i][3]))
+                    __builtin_nontemporal_store(v[i], reinterpret_cast<f4v *>(const_cast<float *>(qrow<true>(yb, rowk, ld_y, 4 * q))));
+                else bad |= 1u << i;
+            }
+        }
+        // non-finite guard (see csr_refix): the row's four outputs recomputed from its CSR row
+        // (v[i] is not read: indexed by a runtime i it would put v in scratch memory)
+        while (bad) {
+            const int i = __builtin_ctz(bad);
+            bad &= bad - 1;
+            const int64_t row = s_row[8 * (wave * RI + i) + r8];
+#pragma unroll 1
+            for (int e = 0; e < 4; ++e)
+                __builtin_nontemporal_store(csr_refix1(xc + e, ld_x, row, csr_ptr, csr_col, csr_val),
+                                            yb + row * ld_y + 4 * q + e);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // One-pass big-clique mixing, register-resident (257..32*R members).  Work item = (clique, 32
 // columns = 128 B of every member row); a block of 16 waves holds the whole item in VGPRs: lane =
@@ -2084,8 +2234,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_mix_bigclique(
 // registers -- each member row is read from HBM ONCE (the two-pass kernel reads it twice).  The
 // clique's metadata (rows, coefficients, residual ranges) is staged in LDS and re-staged only when
 // a block's clique changes: items are clique-major, so a grid-stride block stays on one clique.
-constexpr int kBigRegWaves = 16;
-constexpr int kBigRegCols = 32;
 template <int G, int R, int OCC>
 __global__ __launch_bounds__(kBigRegWaves * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_mix_bigclique_reg(
     const float *__restrict__ x, int64_t ld_x, float *__restrict__ y, int64_t ld_y, int64_t p,
@@ -4232,6 +4380,24 @@ static int launch_bigclique_reg(const float *x, int64_t ld_x, float *y, int64_t 
     int64_t gsz = (int64_t)bpc * cu_count();
     if (gsz > items) gsz = items;
     const dim3 grid((unsigned)gsz), block(kBigRegWaves * 64);
+    // float4 lanes (k_mix_bigclique_v4) on column-blocked slabs whose p, ld and block strides are
+    // multiples of 4 floats, 16-B aligned: the default for one-group cliques (FC-1000, P = 2^20,
+    // same box: 1.355 vs 1.407 ms, profiles/r06/bigclique_v4/); NIIDMIX_BIGREG_V4=0 / 1 turns it
+    // off / on for every group count
+    const char *v4_env = getenv("NIIDMIX_BIGREG_V4");
+    const bool v4 = v4_env ? atoi(v4_env) == 1 : plan->n_groups == 1;
+    if (v4 && p % 4 == 0 && ld_x % 4 == 0 && ld_y % 4 == 0 && bs_x % 4 == 0 &&
+        bs_y % 4 == 0 && aligned16(x) && aligned16(y) && bc_shift < 62 &&
+        bs_x * 4 <= (int64_t)0xffffffffLL && bs_y * 4 <= (int64_t)0xffffffffLL) {
+#define NIIDMIX_BIGV4(G, OCC) hipLaunchKernelGGL((k_mix_bigclique_v4<G, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y, contig, plan->csr_ptr, plan->csr_col, plan->csr_val)
+        switch (plan->n_groups) {
+        case 1: NIIDMIX_BIGV4(1, 8); break; case 2: NIIDMIX_BIGV4(2, 4); break;
+        case 3: NIIDMIX_BIGV4(3, 4); break; case 4: NIIDMIX_BIGV4(4, 4); break;
+        default: return set_error(NIIDMIX_EUNSUPPORTED, "n_groups %d not in 1..4", plan->n_groups);
+        }
+#undef NIIDMIX_BIGV4
+        return check_launch("k_mix_bigclique_v4");
+    }
 #define NIIDMIX_BIGREG(G, R, OCC) hipLaunchKernelGGL((k_mix_bigclique_reg<G, R, OCC>), grid, block, 0, s, x, ld_x, y, ld_y, p, plan->n_cliques, plan->clique_ptr, plan->member_row, plan->member_group, plan->coef, plan->res_ptr, plan->res_col, plan->res_val, nch8, bc_shift, bs_x, bs_y, contig, plan->csr_ptr, plan->csr_col, plan->csr_val)
     if (r16) {
         switch (plan->n_groups) {

@@ -581,9 +581,12 @@ def test_bigclique_one_pass(n, size, inter, p, gpu, oracle_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("n,size,inter", [(1000, 1000, "ring"), (1200, 600, "ring"), (2000, 500, "smallworld")])
-def test_bigclique_blocked_layout(n, size, inter, gpu):
+def test_bigclique_blocked_layout(n, size, inter, gpu, oracle_mod, monkeypatch):
     """The one-pass big-clique kernel on column-blocked slabs [P/B, N, B] (B = 256 and 1024, a
-    ragged last block) is bit-identical to the same kernel on the row-major slab."""
+    ragged last block): with 4-B lanes (NIIDMIX_BIGREG_V4=0) bit-identical to the same kernel on
+    the row-major slab; with float4 lanes (k_mix_bigclique_v4, the default for one-group cliques
+    on blocked slabs; =1 forces it for every group count) within the 1e-5 condition-aware
+    tolerance of the oracle -- its column sums add in another order."""
     from niidmix import memory, ops
     from niidmix.generate import dcliques_csr
     csr, cliques = dcliques_csr(n, size, inter, 1337)
@@ -595,8 +598,19 @@ def test_bigclique_blocked_layout(n, size, inter, gpu):
         y = m(x, kernel="clique")
         xb = memory.to_blocked(x, bc)
         yb = memory.empty_blocked(n, p, gpu, bc)
+        monkeypatch.setenv("NIIDMIX_BIGREG_V4", "0")
         m.mix_blocked(xb, yb, p)
         assert torch.equal(memory.from_blocked(yb, p), y)
+        monkeypatch.setenv("NIIDMIX_BIGREG_V4", "1")
+        yb.fill_(float("nan"))
+        m.mix_blocked(xb, yb, p)
+        y4 = memory.from_blocked(yb, p).cpu().numpy()
+        xn = x.cpu().numpy()
+        ref = oracle_mod.mix_exact_c(xn, csr.row_ptr, csr.col, csr.val)
+        bound = oracle_mod.condition_bound(xn, csr.row_ptr, csr.col, csr.val)
+        ok, worst = oracle_mod.check_tolerance(y4, ref, bound, rtol=RTOL)
+        assert ok, (n, inter, p, worst)
+    monkeypatch.delenv("NIIDMIX_BIGREG_V4")
     # partly overlapping blocked slabs in one allocation are refused (Jacobi, d_sgd.py:99-116)
     k, rows, b = yb.shape
     flat = torch.zeros(2 * k * rows * b, device=gpu)
