@@ -56,11 +56,17 @@ case $PART in
 import glob, json, sys
 path = "profiles/traffic.json"
 out = json.load(open(path))
+# the library the parts measured (every bench line of the session carries its hash); a part's
+# other entries are its seed, possibly older than another part's stamps
+libs = {json.load(open(b))["config"]["lib_sha16"] for b in glob.glob(sys.argv[1] + "/bench_*.json")
+        if "e2e" not in b}
+assert len(libs) == 1, libs
+lib = libs.pop()
 for f in sorted(glob.glob(sys.argv[1] + "/traffic_*.json")):
     for k, v in json.load(open(f))["entries"].items():
-        if v != out["entries"].get(k):          # measured by this part (the rest is its seed)
+        if v.get("lib_sha16") == lib and v != out["entries"].get(k):
             out["entries"][k] = v
-            print("stamped", v.get("lib_sha16"), k)
+            print("stamped", lib, k)
 json.dump(out, open(path, "w"), indent=1, sort_keys=True)
 PY
     ;;
